@@ -1,0 +1,144 @@
+/*
+ * quic_pp.h -- C ABI of the MI355X QUIC packet-protection engine (libquicpp.so).
+ *
+ * This is the drop-in boundary for aioquic's per-packet protection path.  The
+ * reference binds that path as a CPython extension, aioquic._crypto
+ * (src/aioquic/_crypto.c, API stub src/aioquic/_crypto.pyi:1-15), called from
+ * src/aioquic/quic/crypto.py:4.  Each entry point below names the reference
+ * function(s) it replaces.  Plain pointers and sizes only: no HIP, torch or
+ * Python types cross this boundary (streams are passed as void*, i.e. a
+ * hipStream_t; NULL = the null stream).
+ *
+ * Threading: a qpp_keytab may be shared between threads for launches; setting
+ * keys and launching on the same slots concurrently is the caller's race (as
+ * with the reference's per-object scratch, _crypto.c:39-42).  A qpp_session is
+ * single-threaded.
+ */
+#ifndef QUIC_PP_H
+#define QUIC_PP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QPP_ABI_VERSION 1
+
+/* cipher suites (quic/crypto.py:12-16 CIPHER_SUITES) */
+#define QPP_AES_128_GCM 0        /* aes-128-gcm + aes-128-ecb header protection */
+#define QPP_AES_256_GCM 1        /* aes-256-gcm + aes-256-ecb header protection */
+#define QPP_CHACHA20_POLY1305 2  /* chacha20-poly1305 + chacha20 header protection */
+
+#define QPP_PACKET_MAX 1500      /* _crypto.c:13 PACKET_LENGTH_MAX */
+#define QPP_TAG_LEN 16           /* _crypto.c:11 AEAD_TAG_LENGTH */
+#define QPP_MAX_HDR 255          /* longest header / associated data the kernels accept */
+
+/* return codes of the API calls */
+#define QPP_OK 0
+#define QPP_E_ARG (-1)           /* bad argument (NULL, n too large, bad slot) */
+#define QPP_E_HIP (-2)           /* a HIP runtime call failed */
+#define QPP_E_NODEV (-3)         /* no usable gfx950 device */
+#define QPP_E_NOMEM (-4)
+
+/* per-packet status codes (qpp_result.status) */
+#define QPP_S_OK 0
+#define QPP_S_LENGTH 1      /* "Invalid payload length" (_crypto.c:126-129,168-171) or sample out of range */
+#define QPP_S_DECRYPT 2     /* "Payload decryption failed" (_crypto.c:148-152) */
+#define QPP_S_KEY_PHASE 3   /* short header whose key-phase bit differs from the slot's
+                               (quic/crypto.py:91-96): caller retries with the next-phase key */
+#define QPP_S_NO_KEY 4      /* slot never installed: KeyUnavailableError (quic/crypto.py:78-79) */
+
+/* descriptor flags */
+#define QPP_F_NO_HP 1u      /* AEAD only (AEAD.encrypt/.decrypt): no header protection, no
+                               packet-number decode, no key-phase check; hdr_len = AAD length */
+
+/* One packet of a batch.  Offsets are byte offsets into the caller's device
+ * buffers; no alignment is required. */
+typedef struct qpp_desc {
+    uint64_t in_off;   /* protect: header then payload; unprotect: the protected packet */
+    uint64_t out_off;  /* protect: header||ciphertext||tag; unprotect: header||plaintext */
+    uint32_t len;      /* protect: payload length; unprotect: packet length (>= pn_off + 20) */
+    uint16_t hdr_len;  /* protect: header (= AAD) length; unprotect: packet-number offset
+                          ("encrypted_offset"), or the AAD length with QPP_F_NO_HP */
+    uint16_t flags;    /* QPP_F_* */
+    uint64_t pn;       /* protect: packet number; unprotect: expected packet number,
+                          or the exact packet number with QPP_F_NO_HP */
+    uint32_t slot;     /* key-table slot */
+    uint32_t rsv;
+} qpp_desc;            /* 40 bytes */
+
+typedef struct qpp_result {
+    uint64_t pn;       /* unprotect: decoded packet number; protect: pn used */
+    uint16_t status;   /* QPP_S_* */
+    uint16_t hdr_len;  /* plain header length (pn_off + pn_len for unprotect) */
+    uint32_t out_len;  /* bytes written at out_off */
+} qpp_result;          /* 16 bytes */
+
+/* Raw key material for one slot, as produced by derive_key_iv_hp
+ * (quic/crypto.py:34-56).  key/hp use 16 bytes for AES-128, 32 otherwise. */
+typedef struct qpp_key_material {
+    uint32_t slot;
+    uint8_t suite;      /* QPP_AES_128_GCM / QPP_AES_256_GCM / QPP_CHACHA20_POLY1305 */
+    uint8_t key_phase;  /* 0/1, compared with bit 2 of a short header */
+    uint8_t rsv[2];
+    uint8_t iv[12];
+    uint8_t key[32];
+    uint8_t hp[32];
+} qpp_key_material;     /* 84 bytes */
+
+typedef struct qpp_keytab qpp_keytab;   /* device-resident expanded keys */
+typedef struct qpp_session qpp_session; /* pinned staging + device buffers + stream */
+
+/* library / device */
+int qpp_abi_version(void);
+const char *qpp_strerror(int rc);
+int qpp_device_check(void);             /* QPP_OK if the current device is gfx950 */
+
+/* Key tables.  qpp_keytab_set replaces AEAD_init (_crypto.c:68-102) and
+ * HeaderProtection_init (_crypto.c:232-266): one device launch expands AES
+ * round keys, H = E_K(0^128) and the GHASH tables for every slot in km. */
+int qpp_keytab_create(uint32_t capacity, qpp_keytab **out);
+void qpp_keytab_destroy(qpp_keytab *kt);
+uint32_t qpp_keytab_capacity(const qpp_keytab *kt);
+int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void *stream);
+int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *stream);
+
+/* Batched packet protection on device buffers (asynchronous on `stream`).
+ * qpp_protect replaces AEAD_encrypt (_crypto.c:157-194) + HeaderProtection_apply
+ * (_crypto.c:289-319), i.e. CryptoContext.encrypt_packet (quic/crypto.py:105-116).
+ * qpp_unprotect replaces HeaderProtection_remove (_crypto.c:321-350) +
+ * decode_packet_number (quic/packet.py:118-132) + AEAD_decrypt (_crypto.c:115-155),
+ * i.e. CryptoContext.decrypt_packet (quic/crypto.py:75-103).
+ * Packets with the same slot should be contiguous for speed (any order is correct). */
+int qpp_protect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n, const uint8_t *d_in,
+                uint8_t *d_out, qpp_result *d_res, void *stream);
+int qpp_unprotect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
+                  const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream);
+
+/* Header-protection masks: replaces HeaderProtection_mask (_crypto.c:278-287).
+ * d_samples: n x 16 bytes, d_masks: n x 16 bytes (first 5 used). */
+int qpp_hp_mask(const qpp_keytab *kt, const uint32_t *d_slots, const uint8_t *d_samples,
+                uint32_t n, uint8_t *d_masks, void *stream);
+
+/* Synchronous host-buffer forms (pinned staging, H2D, kernel, D2H), used by the
+ * per-packet object API and the end-to-end measurement. */
+int qpp_session_create(size_t max_bytes, uint32_t max_packets, qpp_session **out);
+void qpp_session_destroy(qpp_session *s);
+void *qpp_session_stream(qpp_session *s);
+int qpp_session_protect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc, uint32_t n,
+                        const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len,
+                        qpp_result *res);
+int qpp_session_unprotect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc,
+                          uint32_t n, const uint8_t *in, size_t in_len, uint8_t *out,
+                          size_t out_len, qpp_result *res);
+int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *slots,
+                        const uint8_t *samples, uint32_t n, uint8_t *masks);
+int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material *km,
+                         uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

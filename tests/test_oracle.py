@@ -1,0 +1,105 @@
+"""The CPU oracle pinned against the RFC 9001 / RFC 9369 vectors (the same ones
+aioquic's tests/test_crypto_v1.py and test_crypto_v2.py assert) and against the
+golden vectors generated from the reference's compiled _crypto.c."""
+
+import pytest
+
+from tests.rfc import ALL
+
+AES128, AES256, CHACHA = 0, 1, 2
+
+
+@pytest.mark.parametrize("v", ALL, ids=lambda v: v.tag)
+def test_derive_key_iv_hp(oracle, v):
+    for secret, key, iv, hp in (v.derive_client, v.derive_server):
+        assert oracle.derive_key_iv_hp(AES128, secret, v.version) == (key, iv, hp)
+    secret, key, iv, hp = v.derive_chacha
+    assert oracle.derive_key_iv_hp(CHACHA, secret, v.version) == (key, iv, hp)
+
+
+def _initial(oracle, v, client):
+    cs, ss = oracle.initial_secrets(v.cid, v.version)
+    return oracle.derive_key_iv_hp(AES128, cs if client else ss, v.version)
+
+
+@pytest.mark.parametrize("v", ALL, ids=lambda v: v.tag)
+def test_initial_vectors(oracle, v):
+    ck = _initial(oracle, v, True)
+    sk = _initial(oracle, v, False)
+    out = oracle.protect(AES128, *ck, v.long_client_plain_header, v.long_client_plain_payload,
+                         v.long_client_packet_number)
+    assert out == v.long_client_encrypted_packet
+    out = oracle.protect(AES128, *sk, v.long_server_plain_header, v.long_server_plain_payload,
+                         v.long_server_packet_number)
+    assert out == v.long_server_encrypted_packet
+    h, p, pn = oracle.unprotect(AES128, *ck, v.long_client_encrypted_packet, 18, 0)
+    assert (h, p, pn) == (v.long_client_plain_header, v.long_client_plain_payload,
+                          v.long_client_packet_number)
+    h, p, pn = oracle.unprotect(AES128, *sk, v.long_server_encrypted_packet, 18, 0)
+    assert (h, p, pn) == (v.long_server_plain_header, v.long_server_plain_payload,
+                          v.long_server_packet_number)
+
+
+@pytest.mark.parametrize("v", ALL, ids=lambda v: v.tag)
+def test_short_and_chacha_vectors(oracle, v):
+    k = oracle.derive_key_iv_hp(AES128, v.short_secret, v.version)
+    out = oracle.protect(AES128, *k, v.short_server_plain_header, v.short_server_plain_payload,
+                         v.short_server_packet_number)
+    assert out == v.short_server_encrypted_packet
+    assert oracle.unprotect(AES128, *k, out, 9, 0) == (
+        v.short_server_plain_header, v.short_server_plain_payload, v.short_server_packet_number)
+    k = oracle.derive_key_iv_hp(CHACHA, v.chacha_secret, v.version)
+    out = oracle.protect(CHACHA, *k, v.chacha20_client_plain_header,
+                         v.chacha20_client_plain_payload, v.chacha20_client_packet_number)
+    assert out == v.chacha20_client_encrypted_packet
+    assert oracle.unprotect(CHACHA, *k, out, 1, v.chacha20_client_packet_number) == (
+        v.chacha20_client_plain_header, v.chacha20_client_plain_payload,
+        v.chacha20_client_packet_number)
+
+
+def test_tamper_detected(oracle):
+    import os
+    key, iv, hp = os.urandom(16), os.urandom(12), os.urandom(16)
+    hdr = bytes([0x41]) + os.urandom(8) + b"\x00\x07"
+    pkt = oracle.protect(AES128, key, iv, hp, hdr, os.urandom(100), 7)
+    bad = bytearray(pkt)
+    bad[50] ^= 1
+    with pytest.raises(ValueError, match="decrypt"):
+        oracle.unprotect(AES128, key, iv, hp, bytes(bad), 9, 7)
+
+
+def test_decode_pn(oracle):
+    # RFC 9000 App. A.3 example
+    assert oracle.decode_pn(0x9B32, 16, 0xA82F30EA) == 0xA82F9B32
+    assert oracle.decode_pn(0xFF, 8, 0x100) == 0xFF
+    assert oracle.decode_pn(0x00, 8, 0xFF) == 0x100
+    assert oracle.decode_pn(1, 8, 0) == 1
+
+
+def test_oracle_against_reference_golden(oracle):
+    from tests.golden_util import case_inputs, load_cases, matches, tamper
+
+    cases = load_cases()
+    assert len(cases) > 150
+    for c in cases:
+        x = case_inputs(c, oracle)
+        send_key, send_iv = (x["next_key"], x["next_iv"]) if c["send_phase"] else (x["key"], x["iv"])
+        pkt = oracle.protect(x["suite"], send_key, send_iv, x["hp"], x["header"], x["payload"],
+                             c["pn"])
+        assert matches(c["protected"], pkt), c["seed"]
+        wire = tamper(c, pkt)
+        exp = c["unprotect"]
+        # the reference switches to the next-phase key on a key-phase mismatch
+        first = bytes.fromhex(exp["header"])[0] if exp["ok"] else None
+        use_next = bool(exp.get("phase_flip"))
+        k, iv = (x["next_key"], x["next_iv"]) if use_next else (x["key"], x["iv"])
+        try:
+            h, p, pn = oracle.unprotect(x["suite"], k, iv, x["hp"], wire, c["pn_off"],
+                                        c["expected_pn"])
+        except ValueError as e:
+            assert not exp["ok"], (c["seed"], e)
+            assert exp["error"] == "Payload decryption failed"
+            continue
+        assert exp["ok"], c["seed"]
+        assert h.hex() == exp["header"] and pn == exp["pn"] and matches(exp["payload"], p)
+        assert first is not None
