@@ -1,0 +1,124 @@
+"""Batch engine: protect / unprotect many packets per launch.
+
+The per-packet API (aioquic_amd.crypto) issues one launch per packet to stay
+call-compatible with aioquic.  Real throughput comes from handing the GPU a
+whole batch -- every datagram of a ``datagrams_to_send`` call, or every
+datagram a server socket read -- as one descriptor array.  This module is that
+interface over device-resident buffers (torch tensors on ``cuda``), plus host
+helpers that lay out synthetic or real packets into the descriptor format.
+
+Layout (include/quic_pp.h):
+  desc     n x 40 B  (in_off, out_off, len, hdr_len, flags, pn, slot)
+  results  n x 16 B  (pn, status, hdr_len, out_len)
+  keys     one device table of expanded key slots (KeyTable)
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import layout as L
+from . import _crypto
+
+__all__ = ["PacketEngine", "KeySpec", "layout_packets"]
+
+
+@dataclass
+class KeySpec:
+    slot: int
+    suite: int
+    key: bytes
+    iv: bytes
+    hp: bytes
+    key_phase: int = 0
+
+
+def _ptr(t) -> int:
+    return int(t.data_ptr())
+
+
+class PacketEngine:
+    """Device key table + launches on device buffers.
+
+    Buffers are torch.uint8 CUDA tensors (or anything with ``data_ptr()``).
+    Calls are asynchronous on ``stream`` (default: torch's current stream).
+    """
+
+    def __init__(self, capacity: int):
+        self.table = _crypto.KeyTable(int(capacity))
+
+    @property
+    def capacity(self) -> int:
+        return self.table.capacity
+
+    def set_keys(self, specs) -> None:
+        recs = np.concatenate(
+            [L.key_material(s.slot, s.suite, s.key, s.iv, s.hp, s.key_phase) for s in specs]
+        )
+        self.table.set(recs.tobytes())
+
+    def set_key_records(self, recs: np.ndarray) -> None:
+        assert recs.dtype == L.KEY_MATERIAL
+        self.table.set(np.ascontiguousarray(recs).tobytes())
+
+    @staticmethod
+    def _stream(stream) -> int:
+        if stream is None:
+            import torch
+
+            return int(torch.cuda.current_stream().cuda_stream)
+        if isinstance(stream, int):
+            return stream
+        return int(stream.cuda_stream)
+
+    def protect(self, desc, n: int, inbuf, outbuf, results, stream=None) -> None:
+        _crypto.protect(self.table, _ptr(desc), int(n), _ptr(inbuf), _ptr(outbuf),
+                        _ptr(results), self._stream(stream))
+
+    def unprotect(self, desc, n: int, inbuf, outbuf, results, stream=None) -> None:
+        _crypto.unprotect(self.table, _ptr(desc), int(n), _ptr(inbuf), _ptr(outbuf),
+                          _ptr(results), self._stream(stream))
+
+    # ----------------------------------------------- host-buffer forms ----
+
+    def protect_host(self, desc: np.ndarray, data, out_len: int):
+        out, res = _crypto.protect_host(self.table, np.ascontiguousarray(desc).tobytes(),
+                                        bytes(data), int(out_len))
+        return np.frombuffer(out, dtype=np.uint8), np.frombuffer(res, dtype=L.RESULT)
+
+    def unprotect_host(self, desc: np.ndarray, data, out_len: int):
+        out, res = _crypto.unprotect_host(self.table, np.ascontiguousarray(desc).tobytes(),
+                                          bytes(data), int(out_len))
+        return np.frombuffer(out, dtype=np.uint8), np.frombuffer(res, dtype=L.RESULT)
+
+
+def layout_packets(headers, payloads, pns, slots, *, align: int = 1, tag_room: bool = True,
+                   flags: int = 0):
+    """Pack (header, payload) pairs into one input buffer and build protect
+    descriptors whose outputs go to the same offsets of an output buffer.
+
+    Returns (inbuf uint8 array, desc array, out_size)."""
+    n = len(headers)
+    desc = np.zeros(n, dtype=L.DESC)
+    sizes = [len(h) + len(p) + (L.TAG_LEN if tag_room else 0) for h, p in zip(headers, payloads)]
+    offs = np.zeros(n, dtype=np.int64)
+    pos = 0
+    for i, s in enumerate(sizes):
+        pos = (pos + align - 1) // align * align
+        offs[i] = pos
+        pos += s
+    buf = np.zeros(pos + 16, dtype=np.uint8)
+    for i, (h, p) in enumerate(zip(headers, payloads)):
+        o = int(offs[i])
+        buf[o : o + len(h)] = np.frombuffer(h, dtype=np.uint8)
+        buf[o + len(h) : o + len(h) + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    desc["in_off"] = offs
+    desc["out_off"] = offs
+    desc["len"] = [len(p) for p in payloads]
+    desc["hdr_len"] = [len(h) for h in headers]
+    desc["pn"] = np.asarray(pns, dtype=np.uint64)
+    desc["slot"] = np.asarray(slots, dtype=np.uint32)
+    desc["flags"] = flags
+    return buf, desc, pos + 16

@@ -1,0 +1,271 @@
+// qpp_device.h -- device-side building blocks of the MI355X packet-protection
+// engine: AES (T-table in LDS, one table replicated per LDS bank), GHASH by
+// 4-bit windowed tables in LDS, ChaCha20 and Poly1305 in VALU, and the
+// unaligned byte-stream helpers.  gfx950 only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/quic_pp.h"
+
+namespace qpp {
+
+// ---------------------------------------------------------------- tables --
+
+// AES S-box and the little-endian round table Te0 (byte r of a word = row r):
+// Te0[x] = 2S(x) | S(x)<<8 | S(x)<<16 | 3S(x)<<24.  Generated at compile time
+// from GF(2^8) arithmetic (FIPS-197 sec. 5.1.1), so no table is transcribed.
+struct AesTables {
+    uint8_t sbox[256];
+    uint32_t te0[256];
+};
+
+constexpr uint8_t gf8_mul(uint8_t a, uint8_t b)
+{
+    uint8_t r = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1) r ^= a;
+        a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+        b >>= 1;
+    }
+    return r;
+}
+
+constexpr AesTables make_aes_tables()
+{
+    AesTables t{};
+    for (int x = 0; x < 256; ++x) {
+        // inverse = x^254 in GF(2^8) (0 maps to 0)
+        uint8_t inv = 1, base = (uint8_t)x;
+        for (int e = 254; e; e >>= 1) {
+            if (e & 1) inv = gf8_mul(inv, base);
+            base = gf8_mul(base, base);
+        }
+        uint8_t s = inv;
+        for (int i = 1; i <= 4; ++i) s ^= (uint8_t)((inv << i) | (inv >> (8 - i)));
+        s ^= 0x63;
+        t.sbox[x] = s;
+        t.te0[x] = (uint32_t)gf8_mul(s, 2) | (uint32_t)s << 8 | (uint32_t)s << 16 |
+                   (uint32_t)gf8_mul(s, 3) << 24;
+    }
+    return t;
+}
+
+constexpr AesTables kAesTables = make_aes_tables();
+extern __constant__ AesTables c_aes;
+
+// -------------------------------------------------------------- key slots --
+
+// One expanded key slot (512 bytes).  Words are little-endian views of the
+// byte strings, so packet bytes are used as loaded, with no byte swapping.
+struct KeySlot {
+    uint32_t suite;      // QPP_AES_128_GCM / QPP_AES_256_GCM / QPP_CHACHA20_POLY1305; 0xff = empty
+    uint32_t key_phase;
+    uint32_t nr;         // AES rounds (10 / 14)
+    uint32_t rsv;
+    uint32_t iv[4];      // iv[3] = 0
+    uint32_t rk[60];     // AEAD: AES round keys, or the ChaCha20 key in rk[0..7]
+    uint32_t hrk[60];    // header protection: AES round keys, or the ChaCha20 HP key
+};
+static_assert(sizeof(KeySlot) == 512, "KeySlot layout");
+
+// GHASH tables of one slot: [power p = H^(p+1)][window w][nibble v] -> 16 bytes.
+// Window w = 2*byte + (0: low nibble, 1: high nibble).  32 KiB per slot.
+constexpr int kGhashPowers = 4;
+constexpr int kGhashTabBytes = kGhashPowers * 32 * 16 * 16;
+
+// ---------------------------------------------------------------- helpers --
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ u32x4 xor3(u32x4 a, u32x4 b, u32x4 c)
+{
+    return u32x4{xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
+                 xor3(a.w, b.w, c.w)};
+}
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n)
+{
+    return __builtin_amdgcn_alignbit(x, x, (32 - n) & 31);
+}
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// Unaligned 16-byte global load/store (gfx950 runs with unaligned access on).
+__device__ __forceinline__ u32x4 ld16(const uint8_t *p)
+{
+    u32x4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+__device__ __forceinline__ void st16(uint8_t *p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
+
+// First n (0..16) bytes of p, zero padded.  Only the tail block of a region
+// takes the byte loop.
+__device__ __forceinline__ u32x4 ld_part(const uint8_t *p, int n)
+{
+    if (n >= 16) return ld16(p);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int i = 0; i < n; ++i) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+__device__ __forceinline__ void st_part(uint8_t *p, u32x4 v, int n)
+{
+    if (n >= 16) { st16(p, v); return; }
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int i = 0; i < n; ++i) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+}
+// keep only the first n bytes (GHASH / Poly1305 zero padding)
+__device__ __forceinline__ u32x4 keep_bytes(u32x4 v, int n)
+{
+    if (n >= 16) return v;
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int b = n - 4 * k;
+        uint32_t m = b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1));
+        w[k] &= m;
+    }
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+__device__ __forceinline__ uint32_t byte_of(u32x4 v, int i)
+{
+    uint32_t w = (i < 4) ? v.x : (i < 8) ? v.y : (i < 12) ? v.z : v.w;
+    return (w >> (8 * (i & 3))) & 0xff;
+}
+
+// DPP within a quad of lanes (the 4 lanes that share one packet).
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+constexpr int kQuadSwap1 = 0xB1;  // [1,0,3,2]
+constexpr int kQuadSwap2 = 0x4E;  // [2,3,0,1]
+__device__ __forceinline__ u32x4 quad_xor_all(u32x4 v)
+{
+    v.x ^= quad_perm<kQuadSwap1>(v.x);
+    v.y ^= quad_perm<kQuadSwap1>(v.y);
+    v.z ^= quad_perm<kQuadSwap1>(v.z);
+    v.w ^= quad_perm<kQuadSwap1>(v.w);
+    v.x ^= quad_perm<kQuadSwap2>(v.x);
+    v.y ^= quad_perm<kQuadSwap2>(v.y);
+    v.z ^= quad_perm<kQuadSwap2>(v.z);
+    v.w ^= quad_perm<kQuadSwap2>(v.w);
+    return v;
+}
+
+// ------------------------------------------------------------------- AES --
+
+// T-table lookups.  The LDS copy of Te0 is replicated 32 times so that lane l
+// always reads bank (l & 31): entry x of copy c lives at byte x*128 + c*4.
+// `lo` = (lane & 31) * 4.  For every byte position the address is one shift
+// and one and-or.
+struct LdsTe {
+    const uint32_t *te;  // LDS base
+    uint32_t lo;
+    __device__ __forceinline__ uint32_t b0(uint32_t s) const
+    {
+        return *(const uint32_t *)((const uint8_t *)te + (((s << 7) & 0x7f80u) | lo));
+    }
+    __device__ __forceinline__ uint32_t b1(uint32_t s) const
+    {
+        return *(const uint32_t *)((const uint8_t *)te + (((s >> 1) & 0x7f80u) | lo));
+    }
+    __device__ __forceinline__ uint32_t b2(uint32_t s) const
+    {
+        return *(const uint32_t *)((const uint8_t *)te + (((s >> 9) & 0x7f80u) | lo));
+    }
+    __device__ __forceinline__ uint32_t b3(uint32_t s) const
+    {
+        return *(const uint32_t *)((const uint8_t *)te + (((s >> 17) & 0x7f80u) | lo));
+    }
+};
+
+// Constant-memory lookups (key setup and other cold paths).
+struct ConstTe {
+    __device__ __forceinline__ uint32_t b0(uint32_t s) const { return c_aes.te0[s & 255]; }
+    __device__ __forceinline__ uint32_t b1(uint32_t s) const { return c_aes.te0[(s >> 8) & 255]; }
+    __device__ __forceinline__ uint32_t b2(uint32_t s) const { return c_aes.te0[(s >> 16) & 255]; }
+    __device__ __forceinline__ uint32_t b3(uint32_t s) const { return c_aes.te0[s >> 24]; }
+};
+
+// One AES encryption, state and round keys as little-endian column words.
+// Round: column c takes row r from column c+r (ShiftRows) through Te0 rotated
+// left by 8r (MixColumns coefficients).  Final round keeps S(x), found in
+// bytes 1 and 2 of Te0[x].
+template <int NR, class TE>
+__device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, const TE &T)
+{
+    uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        const uint32_t *k = rk + 4 * r;
+        uint32_t t0 = xor3(xor3(T.b0(s0), rotl(T.b1(s1), 8), rotl(T.b2(s2), 16)),
+                           rotl(T.b3(s3), 24), k[0]);
+        uint32_t t1 = xor3(xor3(T.b0(s1), rotl(T.b1(s2), 8), rotl(T.b2(s3), 16)),
+                           rotl(T.b3(s0), 24), k[1]);
+        uint32_t t2 = xor3(xor3(T.b0(s2), rotl(T.b1(s3), 8), rotl(T.b2(s0), 16)),
+                           rotl(T.b3(s1), 24), k[2]);
+        uint32_t t3 = xor3(xor3(T.b0(s3), rotl(T.b1(s0), 8), rotl(T.b2(s1), 16)),
+                           rotl(T.b3(s2), 24), k[3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint32_t *k = rk + 4 * NR;
+    auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t key) {
+        return (((T.b0(a) >> 8) & 0xffu) | (T.b1(b) & 0xff00u) | (T.b2(c) & 0xff0000u) |
+                ((T.b3(d) << 8) & 0xff000000u)) ^ key;
+    };
+    return u32x4{fin(s0, s1, s2, s3, k[0]), fin(s1, s2, s3, s0, k[1]),
+                 fin(s2, s3, s0, s1, k[2]), fin(s3, s0, s1, s2, k[3])};
+}
+
+// --------------------------------------------------------------- GHASH ----
+
+// x * H^p using the 32 windowed tables of power p at LDS byte offset `tab`.
+// Entry address = tab + w*256 + v*16: the w*256 part folds into the ds_read
+// immediate; (word & 0xF0F0F0F0) already holds high-nibble*16 per byte.
+__device__ __forceinline__ u32x4 ghash_mul(u32x4 x, const uint8_t *lds, uint32_t tab)
+{
+    u32x4 acc = {0, 0, 0, 0};
+    uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t hi = xw[d] & 0xF0F0F0F0u;
+        uint32_t lo = (xw[d] << 4) & 0xF0F0F0F0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int wlo = 2 * (4 * d + b), whi = wlo + 1;
+            uint32_t alo = __builtin_amdgcn_ubfe(lo, 8 * b, 8);
+            uint32_t ahi = __builtin_amdgcn_ubfe(hi, 8 * b, 8);
+            u32x4 e0 = *(const u32x4 *)(lds + tab + wlo * 256 + alo);
+            u32x4 e1 = *(const u32x4 *)(lds + tab + whi * 256 + ahi);
+            acc = xor3(acc, e0, e1);
+        }
+    }
+    return acc;
+}
+
+// Bit-serial GF(2^128) multiply (SP 800-38D Algorithm 1) on little-endian
+// word views; key setup only.
+__device__ inline u32x4 gf128_mul_slow(u32x4 x, u32x4 y)
+{
+    uint64_t xh = (uint64_t)bswap(x.x) << 32 | bswap(x.y), xl = (uint64_t)bswap(x.z) << 32 | bswap(x.w);
+    uint64_t vh = (uint64_t)bswap(y.x) << 32 | bswap(y.y), vl = (uint64_t)bswap(y.z) << 32 | bswap(y.w);
+    uint64_t zh = 0, zl = 0;
+    for (int i = 0; i < 128; ++i) {
+        uint64_t bit = i < 64 ? (xh >> (63 - i)) & 1 : (xl >> (127 - i)) & 1;
+        if (bit) { zh ^= vh; zl ^= vl; }
+        uint64_t lsb = vl & 1;
+        vl = (vl >> 1) | (vh << 63);
+        vh >>= 1;
+        if (lsb) vh ^= 0xe100000000000000ull;
+    }
+    return u32x4{bswap((uint32_t)(zh >> 32)), bswap((uint32_t)zh), bswap((uint32_t)(zl >> 32)),
+                 bswap((uint32_t)zl)};
+}
+
+}  // namespace qpp

@@ -1,0 +1,874 @@
+// qpp_engine.hip -- MI355X (gfx950) QUIC packet-protection kernels.
+//
+// Replaces aioquic's per-packet path (src/aioquic/_crypto.c AEAD_encrypt :157,
+// AEAD_decrypt :115, HeaderProtection_apply :289 / remove :321 / mask :278, and
+// quic/crypto.py CryptoContext.encrypt_packet :105 / decrypt_packet :75) with
+// batched kernels.  Design:
+//   * 4 lanes per packet ("quad"), 64 packets per 256-thread workgroup.
+//     Lane j of a quad owns GHASH/CTR blocks v = 4k + j at step k, where the
+//     block sequence [AAD | CT | lengths] is front-padded to a multiple of 4.
+//     AES-CTR of block v and its GHASH term live in the same lane, so no data
+//     moves between lanes until the final 2-step DPP xor of the tag.
+//   * GHASH: Horner with H^4 per lane, H^(4-j) on the last step; products via
+//     4-bit windowed tables (32 windows x 16 entries x 16 B per power, 32 KiB
+//     for H^1..H^4) in LDS.  Every lane reads window w of the same table at
+//     once and a window is exactly one 256-byte LDS bank row: conflict-free.
+//   * AES: Te0 replicated 32x in LDS (lane l reads bank l&31: conflict-free),
+//     round keys in SGPRs (a workgroup works key slot by key slot).
+//   * ChaCha20-Poly1305: lane j owns 64-byte chunks c = 4k + j; Poly1305 by
+//     per-lane Horner (r per block, r^12 more between chunks) and one DPP sum.
+//   * No MFMA: the work is byte/bit arithmetic, bound by LDS and VALU issue.
+#include <hip/hip_runtime.h>
+
+#include "qpp_chacha.h"
+#include "qpp_device.h"
+
+namespace qpp {
+
+__constant__ AesTables c_aes = kAesTables;
+
+constexpr int kWG = 256;
+constexpr int kPktPerWG = kWG / 4;
+constexpr int kScratch = 48;  // (ct||tag)[0..48) per packet, for the HP sample
+constexpr uint32_t kNoSlot = 0xffffffffu;
+
+struct __attribute__((aligned(16))) Smem {
+    uint32_t te[256 * 32];            // Te0 x 32 bank copies   32 KiB
+    uint8_t gt[kGhashTabBytes];       // GHASH H^1..H^4 tables   32 KiB
+    uint8_t scratch[kPktPerWG][kScratch];
+    uint32_t cur_slot;
+};
+
+__device__ __forceinline__ void load_te(Smem &sm)
+{
+    for (int i = threadIdx.x; i < 256 * 8; i += kWG) {
+        uint32_t v = c_aes.te0[i >> 3];
+        *(u32x4 *)&sm.te[(i >> 3) * 32 + (i & 7) * 4] = u32x4{v, v, v, v};
+    }
+}
+
+// ------------------------------------------------------- packet numbers --
+
+// decode_packet_number (quic/packet.py:118-132).  Bit-exact with the
+// reference, which receives the truncated number from HeaderProtection.remove
+// as a SIGNED int (_crypto.c:349): a 4-byte value >= 2^31 is negative there.
+__device__ __forceinline__ uint64_t decode_pn(uint32_t trunc, int pn_len, uint64_t expected,
+                                              bool rfc)
+{
+    if (pn_len == 4 && trunc >= 0x80000000u && !rfc)
+        return expected >= (uint64_t)trunc - 0x80000000ull ? (uint64_t)trunc
+                                                            : (0xffffffff00000000ull | trunc);
+    const uint64_t window = 1ull << (8 * pn_len), half = window >> 1;
+    const uint64_t cand = (expected & ~(window - 1)) | trunc;
+    if (expected >= half && cand <= expected - half && cand < (1ull << 62) - window)
+        return cand + window;
+    if (cand > expected + half && cand >= window) return cand - window;
+    return cand;
+}
+
+// XOR pattern that (un)masks header bytes [base, base+16): first byte with
+// mask[0] & (0x0f long / 0x1f short), packet number bytes with mask[1..pn_len]
+// (_crypto.c:308-316, :337-347).
+__device__ __forceinline__ u32x4 hp_pattern(int base, u32x4 mask, uint32_t fb_mask, int pn_off,
+                                            int pn_len)
+{
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int pos = base + j, q = pos - pn_off;
+        uint32_t m = 0;
+        if (pos == 0) m = byte_of(mask, 0) & fb_mask;
+        if (q >= 0 && q < pn_len) m = byte_of(mask, 1 + q);
+        w[j >> 2] |= m << (8 * (j & 3));
+    }
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ uint32_t first_byte_mask(uint32_t b0) { return (b0 & 0x80) ? 0x0f : 0x1f; }
+
+// 16 bytes at byte offset s (0..3) of an LDS scratch line
+__device__ __forceinline__ u32x4 lds_sample(const uint8_t *scr, int s)
+{
+    const uint32_t *w = (const uint32_t *)scr;
+    uint32_t a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+    return u32x4{__builtin_amdgcn_alignbyte(b, a, s), __builtin_amdgcn_alignbyte(c, b, s),
+                 __builtin_amdgcn_alignbyte(d, c, s), __builtin_amdgcn_alignbyte(e, d, s)};
+}
+
+template <class TE>
+__device__ __forceinline__ u32x4 hp_mask_of(const KeySlot *ks, uint32_t suite, u32x4 sample,
+                                            const TE &T)
+{
+    if (suite == QPP_CHACHA20_POLY1305) {
+        uint32_t blk[16];
+        chacha_block(ks->hrk, sample.x, sample.y, sample.z, sample.w, blk);
+        return u32x4{blk[0], blk[1], blk[2], blk[3]};
+    }
+    if (suite == QPP_AES_256_GCM) return aes_encrypt<14>(sample, ks->hrk, T);
+    return aes_encrypt<10>(sample, ks->hrk, T);
+}
+
+// -------------------------------------------------------- per-packet view --
+
+struct Pkt {
+    const uint8_t *src;
+    uint8_t *dst;
+    int hlen, clen;         // header/AAD length, ciphertext length
+    int pn_off, pn_len;
+    uint32_t fbm;           // first-byte mask bits
+    uint32_t status;
+    uint64_t pn;
+    bool hp;
+    u32x4 mask;             // header-protection mask (unprotect: known up front)
+    u32x4 nonce;            // iv ^ pn, with word 3 = 0
+};
+
+// Header analysis shared by both suites.  Unprotect removes header
+// protection here (it decides the header length and the packet number).
+template <bool ENC, class TE>
+__device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const uint8_t *gin, uint8_t *gout,
+                                         const KeySlot *ks, uint32_t suite, const TE &T)
+{
+    Pkt P;
+    P.src = gin + d.in_off;
+    P.dst = gout + d.out_off;
+    P.hp = !(d.flags & QPP_F_NO_HP);
+    P.status = QPP_S_OK;
+    P.pn = d.pn;
+    P.mask = u32x4{0, 0, 0, 0};
+    P.pn_off = 0;
+    P.pn_len = 0;
+    P.fbm = 0;
+    P.hlen = 0;
+    P.clen = 0;
+    if (ENC) {
+        P.hlen = d.hdr_len;
+        P.clen = (int)d.len;
+        if (P.clen > QPP_PACKET_MAX || P.hlen > QPP_MAX_HDR) P.status = QPP_S_LENGTH;
+        if (P.hp) {
+            // CryptoContext.encrypt_packet -> HeaderProtection.apply (_crypto.c:298-302)
+            if (P.hlen < 1) {
+                P.status = QPP_S_LENGTH;
+            } else {
+                uint32_t b0 = P.src[0];
+                P.pn_len = (int)(b0 & 3) + 1;
+                P.pn_off = P.hlen - P.pn_len;
+                P.fbm = first_byte_mask(b0);
+                if (P.pn_off < 0 || P.clen + QPP_TAG_LEN < 20 - P.pn_len) P.status = QPP_S_LENGTH;
+            }
+        }
+    } else if (P.hp) {
+        // HeaderProtection.remove (_crypto.c:321-350) + decode (crypto.py:84-89)
+        P.pn_off = d.hdr_len;
+        const int len = (int)d.len;
+        if (P.pn_off < 1 || P.pn_off + 20 > len || P.pn_off > QPP_MAX_HDR - 4) {
+            P.status = QPP_S_LENGTH;
+        } else {
+            const u32x4 sample = ld16(P.src + P.pn_off + 4);
+            P.mask = hp_mask_of(ks, suite, sample, T);
+            uint32_t b0 = P.src[0];
+            P.fbm = first_byte_mask(b0);
+            b0 ^= byte_of(P.mask, 0) & P.fbm;
+            P.pn_len = (int)(b0 & 3) + 1;
+            const u32x4 pnw = ld16(P.src + P.pn_off);
+            uint32_t trunc = 0;
+            for (int i = 0; i < P.pn_len; ++i)
+                trunc = (trunc << 8) | (byte_of(pnw, i) ^ byte_of(P.mask, 1 + i));
+            P.pn = decode_pn(trunc, P.pn_len, d.pn, d.flags & QPP_F_RFC_PN);
+            P.hlen = P.pn_off + P.pn_len;
+            const int body = len - P.hlen;
+            if (body < QPP_TAG_LEN || body > QPP_PACKET_MAX) P.status = QPP_S_LENGTH;
+            else if (!(b0 & 0x80) && ((b0 >> 2) & 1) != ks->key_phase) P.status = QPP_S_KEY_PHASE;
+            P.clen = body - QPP_TAG_LEN;
+        }
+    } else {
+        // AEAD.decrypt (_crypto.c:115-155): data = in[hdr_len:len]
+        P.hlen = d.hdr_len;
+        const int body = (int)d.len - P.hlen;
+        if (P.hlen > QPP_MAX_HDR || body < QPP_TAG_LEN || body > QPP_PACKET_MAX)
+            P.status = QPP_S_LENGTH;
+        P.clen = body - QPP_TAG_LEN;
+    }
+    // nonce = iv ^ (pn as big-endian in the last 8 bytes) (_crypto.c:173-176)
+    P.nonce = u32x4{ks->iv[0], ks->iv[1] ^ bswap((uint32_t)(P.pn >> 32)),
+                    ks->iv[2] ^ bswap((uint32_t)P.pn), 0};
+    return P;
+}
+
+// Protect: header protection over the finished (ct||tag) and the header write.
+template <class TE>
+__device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, uint32_t suite,
+                                                  int sub, uint8_t *scr, u32x4 tag, const TE &T)
+{
+    // sample = (ct||tag)[4-pn_len : 20-pn_len]; the tag only matters when clen < 20
+    if (P.clen < 32 && sub == 0) {
+        for (int j = 0; j < 16 && P.clen + j < kScratch; ++j)
+            scr[P.clen + j] = (uint8_t)byte_of(tag, j);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const u32x4 sample = lds_sample(scr, 4 - P.pn_len);
+    P.mask = hp_mask_of(ks, suite, sample, T);
+    const int n_a = (P.hlen + 15) >> 4;
+    for (int q = sub; q < n_a; q += 4) {
+        const int nb = min(16, P.hlen - 16 * q);
+        u32x4 h = ld_part(P.src + 16 * q, nb);
+        h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
+        st_part(P.dst + 16 * q, h, nb);
+    }
+}
+
+// --------------------------------------------------------------- AES-GCM --
+
+template <int NR, bool ENC>
+__device__ void gcm_packet(Pkt &P, const KeySlot *ks, uint32_t suite, const uint32_t *rk,
+                           int sub, uint8_t *scr, const uint8_t *lds, const LdsTe &T)
+{
+    const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4;
+    const int n_g = n_a + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
+    const u32x4 j0 = u32x4{P.nonce.x, P.nonce.y, P.nonce.z, 0x01000000u};
+    const uint64_t abits = (uint64_t)P.hlen * 8, cbits = (uint64_t)P.clen * 8;
+    const uint8_t *pin = P.src + P.hlen;
+    uint8_t *pout = P.dst + P.hlen;
+    const bool unmask = !ENC && P.hp;
+    constexpr uint32_t kTabH4 = 3 * 8192;
+    u32x4 acc = {0, 0, 0, 0}, ej0 = {0, 0, 0, 0};
+
+    for (int k = 0; k < S; ++k) {
+        const int g = 4 * k + sub - pad, i = g - n_a;
+        u32x4 ctr = j0;
+        if (i >= 0 && i < n_c) ctr.w = bswap((uint32_t)(i + 2));
+        const u32x4 ksb = aes_encrypt<NR>(ctr, rk, T);
+        u32x4 x = {0, 0, 0, 0};
+        if (g >= 0 && g < n_a) {
+            // associated data = the (plain) header
+            const int nb = min(16, P.hlen - 16 * g);
+            x = ld_part(P.src + 16 * g, nb);
+            if (unmask) x ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
+            if (!ENC || !P.hp) st_part(P.dst + 16 * g, x, nb);
+        } else if (i >= 0 && i < n_c) {
+            const int nb = min(16, P.clen - 16 * i);
+            const u32x4 din = ld_part(pin + 16 * i, nb);
+            const u32x4 dout = din ^ ksb;
+            st_part(pout + 16 * i, dout, nb);
+            x = keep_bytes(ENC ? dout : din, nb);
+            if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x;
+        } else if (i == n_c) {
+            // lengths block; this lane's AES slot produced E_K(J0) for the tag
+            x = u32x4{bswap((uint32_t)(abits >> 32)), bswap((uint32_t)abits),
+                      bswap((uint32_t)(cbits >> 32)), bswap((uint32_t)cbits)};
+            ej0 = ksb;
+        }
+        acc ^= x;
+        if (k < S - 1) acc = ghash_mul(acc, lds, kTabH4);
+        else acc = ghash_mul(acc, lds, (uint32_t)(3 - sub) * 8192u);
+    }
+    const u32x4 tag = quad_xor_all(acc ^ ej0);
+    if (ENC) {
+        if (sub == 0) st16(pout + P.clen, tag);
+        if (P.hp) protect_finish_hp(P, ks, suite, sub, scr, tag, T);
+    } else {
+        const u32x4 got = ld16(pin + P.clen);
+        const u32x4 diff = got ^ tag;
+        if ((diff.x | diff.y | diff.z | diff.w) != 0) P.status = QPP_S_DECRYPT;
+    }
+}
+
+// ---------------------------------------------------- ChaCha20-Poly1305 --
+
+template <bool ENC>
+__device__ void chacha_packet(Pkt &P, const KeySlot *ks, uint32_t suite, int sub, uint8_t *scr,
+                              const LdsTe &T)
+{
+    const uint32_t *key = ks->rk;
+    const uint32_t n0 = P.nonce.x, n1 = P.nonce.y, n2 = P.nonce.z;
+    const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4;
+    const int n_g = n_a + n_c + 1;
+    const int chunks = (P.clen + 63) >> 6;
+    const bool unmask = !ENC && P.hp;
+    const uint8_t *pin = P.src + P.hlen;
+    uint8_t *pout = P.dst + P.hlen;
+
+    // one-time Poly1305 key = ChaCha20(key, counter 0) (RFC 8439 sec. 2.6)
+    uint32_t blk[16];
+    chacha_block(key, 0, n0, n1, n2, blk);
+    const P130 r = p130_r(blk[0], blk[1], blk[2], blk[3]);
+    const uint32_t s0 = blk[4], s1 = blk[5], s2 = blk[6], s3 = blk[7];
+    const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
+    const P130 r12 = p130_mul(r8, r4);
+
+    P130 acc = p130_zero();
+    int g_last = -1;
+    // lane 0 starts its chain with the associated data (Δ = 1 into chunk 0)
+    if (sub == 0) {
+        for (int g = 0; g < n_a; ++g) {
+            const int nb = min(16, P.hlen - 16 * g);
+            u32x4 x = ld_part(P.src + 16 * g, nb);
+            if (unmask) x ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
+            if (!ENC || !P.hp) st_part(P.dst + 16 * g, x, nb);
+            acc = p130_mul(p130_add(acc, p130_block(x)), r);
+            g_last = g;
+        }
+    }
+    // acc already carries one factor r per folded block: h = (h + m) * r
+    for (int c = sub; c < chunks; c += 4) {
+        chacha_block(key, (uint32_t)(1 + c), n0, n1, n2, blk);
+        // jump from this lane's previous block to the first block of chunk c
+        if (g_last >= 0 && c >= 4) acc = p130_mul(acc, r12);  // gap of 13 blocks: r^12, then r^1 per block
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i = 4 * c + t;
+            if (i >= n_c) break;
+            const int nb = min(16, P.clen - 16 * i);
+            const u32x4 din = ld_part(pin + 16 * i, nb);
+            const u32x4 ksb = u32x4{blk[4 * t], blk[4 * t + 1], blk[4 * t + 2], blk[4 * t + 3]};
+            const u32x4 dout = din ^ ksb;
+            st_part(pout + 16 * i, dout, nb);
+            const u32x4 x = keep_bytes(ENC ? dout : din, nb);
+            if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x;
+            acc = p130_mul(p130_add(acc, p130_block(x)), r);
+            g_last = n_a + i;
+        }
+    }
+    // acc = sum m_g r^(g_last - g + 1); scale to r^(n_g - g) with r^(n_g - 1 - g_last)
+    int e = n_g - 1 - g_last;  // >= 1 when this lane holds blocks
+    if (g_last < 0) e = 0;
+    P130 f = acc;
+    if (e > 1) {
+        // square-and-multiply over r^1, r^2, r^4, r^8, r^16 (e <= 17)
+        const int m = e - 1;
+        const P130 r16 = p130_mul(r8, r8);
+        if (m & 1) f = p130_mul(f, r);
+        if (m & 2) f = p130_mul(f, r2);
+        if (m & 4) f = p130_mul(f, r4);
+        if (m & 8) f = p130_mul(f, r8);
+        if (m & 16) f = p130_mul(f, r16);
+    }
+    // sum over the quad (limbs < 2^28 each, no carries needed), add the lengths block
+    P130 sum;
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        uint32_t v = f.v[l];
+        v += quad_perm<kQuadSwap1>(v);
+        v += quad_perm<kQuadSwap2>(v);
+        sum.v[l] = v;
+    }
+    const u32x4 lens = u32x4{(uint32_t)P.hlen, 0u, (uint32_t)P.clen, 0u};
+    sum = p130_mul(p130_add(sum, p130_block(lens)), r);
+    const u32x4 tag = p130_finish(sum, s0, s1, s2, s3);
+    if (ENC) {
+        if (sub == 0) st16(pout + P.clen, tag);
+        if (P.hp) protect_finish_hp(P, ks, suite, sub, scr, tag, T);
+    } else {
+        const u32x4 got = ld16(pin + P.clen);
+        const u32x4 diff = got ^ tag;
+        if ((diff.x | diff.y | diff.z | diff.w) != 0) P.status = QPP_S_DECRYPT;
+    }
+}
+
+// ---------------------------------------------------------------- kernels --
+
+template <bool ENC>
+__global__ __launch_bounds__(kWG) void k_packets(const KeySlot *__restrict__ slots,
+                                                 const uint8_t *__restrict__ gtab, uint32_t cap,
+                                                 const qpp_desc *__restrict__ desc, uint32_t n,
+                                                 const uint8_t *gin, uint8_t *gout,
+                                                 qpp_result *__restrict__ res)
+{
+    __shared__ Smem sm;
+    const int tid = threadIdx.x, sub = tid & 3, lp = tid >> 2;
+    load_te(sm);
+    const uint32_t p = blockIdx.x * kPktPerWG + lp;
+    const bool valid = p < n;
+    qpp_desc d = {};
+    if (valid) d = desc[p];
+    uint32_t my_slot = valid ? d.slot : kNoSlot;
+    bool done = !valid;
+    if (valid && my_slot >= cap) {
+        if (sub == 0) res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+        done = true;
+    }
+    const LdsTe T{sm.te, (uint32_t)(tid & 31) * 4};
+    uint8_t *scr = sm.scratch[lp];
+
+    for (;;) {
+        if (tid == 0) sm.cur_slot = kNoSlot;
+        __syncthreads();
+        if (!done) atomicMin(&sm.cur_slot, my_slot);
+        __syncthreads();
+        const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur_slot);
+        if (cur == kNoSlot) break;
+        const KeySlot *ks = slots + cur;
+        const uint32_t suite = __builtin_amdgcn_readfirstlane(ks->suite);
+        const bool gcm = suite == QPP_AES_128_GCM || suite == QPP_AES_256_GCM;
+        if (gcm) {
+            const u32x4 *src = (const u32x4 *)(gtab + (size_t)cur * kGhashTabBytes);
+            for (int i = tid; i < kGhashTabBytes / 16; i += kWG) ((u32x4 *)sm.gt)[i] = src[i];
+        }
+        __syncthreads();
+        if (!done && my_slot == cur) {
+            done = true;
+            if (suite > QPP_CHACHA20_POLY1305) {
+                if (sub == 0) res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+            } else {
+                Pkt P = pkt_begin<ENC>(d, gin, gout, ks, suite, T);
+                if (P.status == QPP_S_OK) {
+                    if (suite == QPP_AES_128_GCM) {
+                        uint32_t rk[44];
+#pragma unroll
+                        for (int i = 0; i < 44; ++i) rk[i] = __builtin_amdgcn_readfirstlane(ks->rk[i]);
+                        gcm_packet<10, ENC>(P, ks, suite, rk, sub, scr, sm.gt, T);
+                    } else if (suite == QPP_AES_256_GCM) {
+                        uint32_t rk[60];
+#pragma unroll
+                        for (int i = 0; i < 60; ++i) rk[i] = __builtin_amdgcn_readfirstlane(ks->rk[i]);
+                        gcm_packet<14, ENC>(P, ks, suite, rk, sub, scr, sm.gt, T);
+                    } else {
+                        chacha_packet<ENC>(P, ks, suite, sub, scr, T);
+                    }
+                }
+                if (sub == 0) {
+                    const uint32_t out_len =
+                        P.status == QPP_S_OK ? (uint32_t)(P.hlen + P.clen + (ENC ? QPP_TAG_LEN : 0)) : 0u;
+                    res[p] = qpp_result{P.pn, (uint16_t)P.status, (uint16_t)P.hlen, out_len};
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Header-protection masks only (HeaderProtection_mask, _crypto.c:278-287).
+__global__ __launch_bounds__(kWG) void k_hp_mask(const KeySlot *__restrict__ slots, uint32_t cap,
+                                                 const uint32_t *__restrict__ sidx,
+                                                 const uint8_t *__restrict__ samples, uint32_t n,
+                                                 uint8_t *__restrict__ masks)
+{
+    __shared__ Smem sm;
+    load_te(sm);
+    __syncthreads();
+    const LdsTe T{sm.te, (uint32_t)(threadIdx.x & 31) * 4};
+    const uint32_t i = blockIdx.x * kWG + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = sidx[i];
+    u32x4 m = {0, 0, 0, 0};
+    if (s < cap && slots[s].suite <= QPP_CHACHA20_POLY1305)
+        m = hp_mask_of(slots + s, slots[s].suite, ld16(samples + 16 * (size_t)i), T);
+    st16(masks + 16 * (size_t)i, m);
+}
+
+// --------------------------------------------------------------- key setup --
+
+// FIPS-197 sec. 5.2 in little-endian words (RotWord = rotr 8, Rcon in byte 0).
+__device__ int expand_key(const uint8_t *key, int klen, uint32_t *rk)
+{
+    const int nk = klen / 4, nr = nk + 6;
+    for (int i = 0; i < nk; ++i)
+        rk[i] = key[4 * i] | (uint32_t)key[4 * i + 1] << 8 | (uint32_t)key[4 * i + 2] << 16 |
+                (uint32_t)key[4 * i + 3] << 24;
+    uint32_t rcon = 1;
+    auto sub_word = [](uint32_t t) {
+        return (uint32_t)c_aes.sbox[t & 255] | (uint32_t)c_aes.sbox[(t >> 8) & 255] << 8 |
+               (uint32_t)c_aes.sbox[(t >> 16) & 255] << 16 | (uint32_t)c_aes.sbox[t >> 24] << 24;
+    };
+    for (int i = nk; i < 4 * (nr + 1); ++i) {
+        uint32_t t = rk[i - 1];
+        if (i % nk == 0) {
+            t = sub_word((t >> 8) | (t << 24)) ^ rcon;
+            rcon = gf8_mul((uint8_t)rcon, 2);
+        } else if (nk > 6 && i % nk == 4) {
+            t = sub_word(t);
+        }
+        rk[i] = rk[i - nk] ^ t;
+    }
+    return nr;
+}
+
+__device__ __forceinline__ uint32_t le32(const uint8_t *p)
+{
+    return p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+// One workgroup per key: round keys / ChaCha keys, H = E_K(0^128), H^2..H^4
+// and the 2048 GHASH table entries (AEAD_init + HeaderProtection_init).
+__global__ __launch_bounds__(kWG) void k_key_setup(KeySlot *__restrict__ slots,
+                                                   uint8_t *__restrict__ gtab, uint32_t cap,
+                                                   const qpp_key_material *__restrict__ km,
+                                                   uint32_t n)
+{
+    __shared__ KeySlot ks;
+    __shared__ u32x4 hpow[kGhashPowers];
+    const qpp_key_material &m = km[blockIdx.x];
+    if (m.slot >= cap) return;
+    if (threadIdx.x == 0) {
+        ks.suite = m.suite;
+        ks.key_phase = m.key_phase & 1;
+        ks.rsv = 0;
+        for (int i = 0; i < 3; ++i) ks.iv[i] = le32(m.iv + 4 * i);
+        ks.iv[3] = 0;
+        for (int i = 0; i < 60; ++i) ks.rk[i] = ks.hrk[i] = 0;
+        if (m.suite == QPP_CHACHA20_POLY1305) {
+            ks.nr = 0;
+            for (int i = 0; i < 8; ++i) {
+                ks.rk[i] = le32(m.key + 4 * i);
+                ks.hrk[i] = le32(m.hp + 4 * i);
+            }
+        } else {
+            const int klen = m.suite == QPP_AES_256_GCM ? 32 : 16;
+            ks.nr = (uint32_t)expand_key(m.key, klen, ks.rk);
+            expand_key(m.hp, klen, ks.hrk);
+            const ConstTe CT;
+            const u32x4 zero = {0, 0, 0, 0};
+            const u32x4 h = ks.nr == 14 ? aes_encrypt<14>(zero, ks.rk, CT)
+                                        : aes_encrypt<10>(zero, ks.rk, CT);
+            hpow[0] = h;
+            for (int p = 1; p < kGhashPowers; ++p) hpow[p] = gf128_mul_slow(hpow[p - 1], h);
+        }
+    }
+    __syncthreads();
+    KeySlot *dst = slots + m.slot;
+    for (int i = threadIdx.x; i < (int)(sizeof(KeySlot) / 4); i += kWG)
+        ((uint32_t *)dst)[i] = ((const uint32_t *)&ks)[i];
+    if (m.suite == QPP_AES_128_GCM || m.suite == QPP_AES_256_GCM) {
+        u32x4 *tab = (u32x4 *)(gtab + (size_t)m.slot * kGhashTabBytes);
+        for (int e = threadIdx.x; e < kGhashPowers * 32 * 16; e += kWG) {
+            const int p = e >> 9, w = (e >> 4) & 31, v = e & 15;
+            // element with nibble v at window w: byte w/2, low (w even) or high nibble
+            uint32_t words[4] = {0, 0, 0, 0};
+            const int byte = w >> 1;
+            words[byte >> 2] = (uint32_t)(v << (4 * (w & 1))) << (8 * (byte & 3));
+            tab[e] = gf128_mul_slow(u32x4{words[0], words[1], words[2], words[3]}, hpow[p]);
+        }
+    }
+}
+
+__global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, uint32_t cap)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && idx[i] < cap) slots[idx[i]].suite = 0xffu;
+}
+
+}  // namespace qpp
+
+// ======================================================== host: C ABI ======
+
+#include <stdlib.h>
+#include <string.h>
+
+using namespace qpp;
+
+struct qpp_keytab {
+    uint32_t cap;
+    int device;
+    KeySlot *d_slots;
+    uint8_t *d_gtab;
+    qpp_key_material *d_km;
+    uint32_t km_cap;
+};
+
+struct qpp_session {
+    hipStream_t stream;
+    int device;
+    size_t max_bytes;
+    uint32_t max_packets;
+    uint8_t *h_in, *h_out, *h_misc;  // pinned
+    uint8_t *d_in, *d_out, *d_misc;
+    size_t misc_bytes;
+};
+
+#define HIPCHK(x)                          \
+    do {                                   \
+        if ((x) != hipSuccess) {           \
+            (void)hipGetLastError();       \
+            return QPP_E_HIP;              \
+        }                                  \
+    } while (0)
+
+extern "C" {
+
+int qpp_abi_version(void) { return QPP_ABI_VERSION; }
+
+const char *qpp_strerror(int rc)
+{
+    switch (rc) {
+    case QPP_OK: return "ok";
+    case QPP_E_ARG: return "invalid argument";
+    case QPP_E_HIP: return "HIP runtime error";
+    case QPP_E_NODEV: return "no gfx950 device";
+    case QPP_E_NOMEM: return "out of memory";
+    default: return "unknown error";
+    }
+}
+
+int qpp_device_check(void)
+{
+    int dev = 0, count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) {
+        (void)hipGetLastError();
+        return QPP_E_NODEV;
+    }
+    HIPCHK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    return strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? QPP_OK : QPP_E_NODEV;
+}
+
+int qpp_keytab_create(uint32_t capacity, qpp_keytab **out)
+{
+    if (!out || capacity == 0 || capacity > (1u << 24)) return QPP_E_ARG;
+    *out = NULL;
+    int rc = qpp_device_check();
+    if (rc != QPP_OK) return rc;
+    qpp_keytab *kt = (qpp_keytab *)calloc(1, sizeof(qpp_keytab));
+    if (!kt) return QPP_E_NOMEM;
+    kt->cap = capacity;
+    (void)hipGetDevice(&kt->device);
+    if (hipMalloc(&kt->d_slots, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
+        hipMalloc(&kt->d_gtab, (size_t)capacity * kGhashTabBytes) != hipSuccess ||
+        hipMemset(kt->d_slots, 0xff, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+        (void)hipGetLastError();
+        qpp_keytab_destroy(kt);
+        return QPP_E_NOMEM;
+    }
+    *out = kt;
+    return QPP_OK;
+}
+
+void qpp_keytab_destroy(qpp_keytab *kt)
+{
+    if (!kt) return;
+    if (kt->d_slots) (void)hipFree(kt->d_slots);
+    if (kt->d_gtab) (void)hipFree(kt->d_gtab);
+    if (kt->d_km) (void)hipFree(kt->d_km);
+    free(kt);
+}
+
+uint32_t qpp_keytab_capacity(const qpp_keytab *kt) { return kt ? kt->cap : 0; }
+
+int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void *stream)
+{
+    if (!kt || (!km && n)) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (km[i].slot >= kt->cap || km[i].suite > QPP_CHACHA20_POLY1305) return QPP_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (n > kt->km_cap) {
+        if (kt->d_km) HIPCHK(hipFree(kt->d_km));
+        kt->d_km = NULL;
+        kt->km_cap = 0;
+        HIPCHK(hipMalloc(&kt->d_km, (size_t)n * sizeof(qpp_key_material)));
+        kt->km_cap = n;
+    }
+    HIPCHK(hipMemcpyAsync(kt->d_km, km, (size_t)n * sizeof(qpp_key_material),
+                          hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_key_setup, dim3(n), dim3(kWG), 0, s, kt->d_slots, kt->d_gtab, kt->cap,
+                       kt->d_km, n);
+    HIPCHK(hipGetLastError());
+    // key material is host memory owned by the caller: finish before returning
+    HIPCHK(hipStreamSynchronize(s));
+    return QPP_OK;
+}
+
+int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *stream)
+{
+    if (!kt || (!slots && n)) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t *d = NULL;
+    HIPCHK(hipMalloc(&d, (size_t)n * 4));
+    if (hipMemcpyAsync(d, slots, (size_t)n * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+        (void)hipFree(d);
+        return QPP_E_HIP;
+    }
+    hipLaunchKernelGGL(k_clear_slots, dim3((n + 255) / 256), dim3(256), 0, s, kt->d_slots, d, n,
+                       kt->cap);
+    hipError_t e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    return e == hipSuccess ? QPP_OK : QPP_E_HIP;
+}
+
+static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
+                          const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream)
+{
+    if (!kt || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    const dim3 grid((n + kPktPerWG - 1) / kPktPerWG);
+    if (enc)
+        hipLaunchKernelGGL(k_packets<true>, grid, dim3(kWG), 0, (hipStream_t)stream, kt->d_slots,
+                           kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);
+    else
+        hipLaunchKernelGGL(k_packets<false>, grid, dim3(kWG), 0, (hipStream_t)stream, kt->d_slots,
+                           kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);
+    HIPCHK(hipGetLastError());
+    return QPP_OK;
+}
+
+int qpp_protect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n, const uint8_t *d_in,
+                uint8_t *d_out, qpp_result *d_res, void *stream)
+{
+    return launch_packets(true, kt, d_desc, n, d_in, d_out, d_res, stream);
+}
+
+int qpp_unprotect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
+                  const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream)
+{
+    return launch_packets(false, kt, d_desc, n, d_in, d_out, d_res, stream);
+}
+
+int qpp_hp_mask(const qpp_keytab *kt, const uint32_t *d_slots, const uint8_t *d_samples,
+                uint32_t n, uint8_t *d_masks, void *stream)
+{
+    if (!kt || (n && (!d_slots || !d_samples || !d_masks))) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    hipLaunchKernelGGL(k_hp_mask, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, (hipStream_t)stream,
+                       kt->d_slots, kt->cap, d_slots, d_samples, n, d_masks);
+    HIPCHK(hipGetLastError());
+    return QPP_OK;
+}
+
+// ------------------------------------------------------------- sessions --
+
+static void session_free_buffers(qpp_session *s)
+{
+    if (s->h_in) (void)hipHostFree(s->h_in);
+    if (s->h_out) (void)hipHostFree(s->h_out);
+    if (s->h_misc) (void)hipHostFree(s->h_misc);
+    if (s->d_in) (void)hipFree(s->d_in);
+    if (s->d_out) (void)hipFree(s->d_out);
+    if (s->d_misc) (void)hipFree(s->d_misc);
+    s->h_in = s->h_out = s->h_misc = s->d_in = s->d_out = s->d_misc = NULL;
+}
+
+static size_t misc_bytes_for(uint32_t max_packets)
+{
+    // descriptors + results + slot ids + samples + masks
+    return (size_t)max_packets * (sizeof(qpp_desc) + sizeof(qpp_result) + 4 + 16 + 16) + 256;
+}
+
+static int session_reserve(qpp_session *s, size_t bytes, uint32_t packets)
+{
+    if (bytes <= s->max_bytes && packets <= s->max_packets && s->h_in) return QPP_OK;
+    size_t nb = bytes > s->max_bytes ? bytes : s->max_bytes;
+    uint32_t np = packets > s->max_packets ? packets : s->max_packets;
+    if (nb < 4096) nb = 4096;
+    if (np < 64) np = 64;
+    session_free_buffers(s);
+    s->max_bytes = nb;
+    s->max_packets = np;
+    s->misc_bytes = misc_bytes_for(np);
+    if (hipHostMalloc(&s->h_in, nb, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s->h_out, nb, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s->h_misc, s->misc_bytes, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&s->d_in, nb) != hipSuccess || hipMalloc(&s->d_out, nb) != hipSuccess ||
+        hipMalloc(&s->d_misc, s->misc_bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        session_free_buffers(s);
+        s->max_bytes = 0;
+        s->max_packets = 0;
+        return QPP_E_NOMEM;
+    }
+    return QPP_OK;
+}
+
+int qpp_session_create(size_t max_bytes, uint32_t max_packets, qpp_session **out)
+{
+    if (!out) return QPP_E_ARG;
+    *out = NULL;
+    int rc = qpp_device_check();
+    if (rc != QPP_OK) return rc;
+    qpp_session *s = (qpp_session *)calloc(1, sizeof(qpp_session));
+    if (!s) return QPP_E_NOMEM;
+    (void)hipGetDevice(&s->device);
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        free(s);
+        return QPP_E_HIP;
+    }
+    rc = session_reserve(s, max_bytes, max_packets);
+    if (rc != QPP_OK) {
+        qpp_session_destroy(s);
+        return rc;
+    }
+    *out = s;
+    return QPP_OK;
+}
+
+void qpp_session_destroy(qpp_session *s)
+{
+    if (!s) return;
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    session_free_buffers(s);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    free(s);
+}
+
+void *qpp_session_stream(qpp_session *s) { return s ? (void *)s->stream : NULL; }
+
+static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc,
+                       uint32_t n, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len,
+                       qpp_result *res)
+{
+    if (!s || !kt || (n && (!desc || !res))) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    size_t need = in_len > out_len ? in_len : out_len;
+    int rc = session_reserve(s, need, n);
+    if (rc != QPP_OK) return rc;
+    qpp_desc *hd = (qpp_desc *)s->h_misc;
+    qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
+    qpp_desc *dd = (qpp_desc *)s->d_misc;
+    qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
+    memcpy(hd, desc, (size_t)n * sizeof(qpp_desc));
+    if (in_len) memcpy(s->h_in, in, in_len);
+    HIPCHK(hipMemcpyAsync(dd, hd, (size_t)n * sizeof(qpp_desc), hipMemcpyHostToDevice, s->stream));
+    if (in_len) HIPCHK(hipMemcpyAsync(s->d_in, s->h_in, in_len, hipMemcpyHostToDevice, s->stream));
+    rc = launch_packets(enc, kt, dd, n, s->d_in, s->d_out, dr, s->stream);
+    if (rc != QPP_OK) return rc;
+    if (out_len) HIPCHK(hipMemcpyAsync(s->h_out, s->d_out, out_len, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    if (out_len) memcpy(out, s->h_out, out_len);
+    memcpy(res, hr, (size_t)n * sizeof(qpp_result));
+    return QPP_OK;
+}
+
+int qpp_session_protect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc, uint32_t n,
+                        const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len,
+                        qpp_result *res)
+{
+    return session_run(true, s, kt, desc, n, in, in_len, out, out_len, res);
+}
+
+int qpp_session_unprotect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc,
+                          uint32_t n, const uint8_t *in, size_t in_len, uint8_t *out,
+                          size_t out_len, qpp_result *res)
+{
+    return session_run(false, s, kt, desc, n, in, in_len, out, out_len, res);
+}
+
+int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *slots,
+                        const uint8_t *samples, uint32_t n, uint8_t *masks)
+{
+    if (!s || !kt || (n && (!slots || !samples || !masks))) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    int rc = session_reserve(s, (size_t)n * 32, n);
+    if (rc != QPP_OK) return rc;
+    uint8_t *hs = s->h_in, *hm = s->h_out;
+    uint32_t *hidx = (uint32_t *)s->h_misc;
+    memcpy(hidx, slots, (size_t)n * 4);
+    memcpy(hs, samples, (size_t)n * 16);
+    HIPCHK(hipMemcpyAsync(s->d_misc, hidx, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->d_in, hs, (size_t)n * 16, hipMemcpyHostToDevice, s->stream));
+    rc = qpp_hp_mask(kt, (const uint32_t *)s->d_misc, s->d_in, n, s->d_out, s->stream);
+    if (rc != QPP_OK) return rc;
+    HIPCHK(hipMemcpyAsync(hm, s->d_out, (size_t)n * 16, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    memcpy(masks, hm, (size_t)n * 16);
+    return QPP_OK;
+}
+
+int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material *km, uint32_t n)
+{
+    if (!s) return QPP_E_ARG;
+    return qpp_keytab_set(kt, km, n, s->stream);
+}
+
+}  // extern "C"

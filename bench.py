@@ -1,0 +1,287 @@
+"""Benchmark: device-resident QUIC packet protect + unprotect on MI355X.
+
+Metric (BASELINE.json): GiB/s of device-resident AEAD protect+unprotect on
+1200 B packets = packets * 1200 B / (t_protect + t_unprotect), summed over all
+ranks (weak scaling: every rank owns its own shard of packets, no collective
+on the data path).  One "step" = protect the batch, then unprotect it.
+
+Default workload = BASELINE config 2: AES-128-GCM, 64Ki x 1200 B, one key.
+Other configs (--config 3/4/5) are parity/throughput cases of the same path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--e2e]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+
+import argparse
+import glob
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_PKT_KERNEL = 1184 + 1200 + 40 + 16  # algorithmic HBM bytes per packet per kernel
+
+CONFIGS = {
+    2: dict(name="aes-128-gcm 64Ki x 1200B, 1 key", n=65536, suite=0, n_keys=1, version=1),
+    3: dict(name="chacha20-poly1305 64Ki x 1200B, 1 key, QUIC v2", n=65536, suite=2, n_keys=1,
+            version=0x6B3343CF),
+    4: dict(name="aes-256-gcm 1Mi x 1200B, 4096 keys", n=1 << 20, suite=1, n_keys=4096,
+            version=1),
+    5: dict(name="mixed aes-128-gcm/chacha20-poly1305 2Mi x 1200B per GPU", n=1 << 21, suite=0,
+            n_keys=2, version=1, mixed=(0, 2)),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--e2e", action="store_true", help="also time pinned H2D->kernels->D2H")
+    ap.add_argument("--check", action="store_true", help="verify round trip after timing")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------ CPU baseline --
+
+
+def _load_reference():
+    """oracle/_ref: the reference's own _crypto.c, built from /root/reference."""
+    so = glob.glob(os.path.join(ROOT, "oracle", "_ref", "aioquic_ref", "_crypto*.so"))
+    if not so:
+        return None
+    try:
+        spec = importlib.util.spec_from_file_location("_crypto", so[0])
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+    except Exception:
+        return None
+
+
+def cpu_baseline(w, seconds: float, cfg):
+    """Time aioquic's own per-packet path (CryptoContext.encrypt_packet =
+    AEAD.encrypt + HeaderProtection.apply; decrypt_packet = remove +
+    decode_packet_number + AEAD.decrypt, quic/crypto.py:75-116) on one core,
+    over a bounded sample of the same synthetic packets."""
+    from aioquic_amd.packet import decode_packet_number
+
+    names = {0: (b"aes-128-gcm", b"aes-128-ecb", 16), 1: (b"aes-256-gcm", b"aes-256-ecb", 32),
+             2: (b"chacha20-poly1305", b"chacha20", 32)}
+    ref = _load_reference()
+    kind = "reference" if ref is not None else "port"
+    if ref is None:
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as orc
+    k = w.keys[0]
+    suite = int(k["suite"])
+    an, hn, kl = names[suite]
+    key, iv, hp = bytes(k["key"][:kl]), bytes(k["iv"]), bytes(k["hp"][:kl])
+    m = min(w.n, 20000)
+    pk = [bytes(w.plain[i * 1200 : i * 1200 + 1184]) for i in range(m)]
+    pns = [int(x) for x in w.desc["pn"][:m]]
+    done = 0
+    t_p = t_u = 0.0
+    t_end = time.perf_counter() + seconds
+    if ref is not None:
+        aead = ref.AEAD(an, key, iv)
+        hpo = ref.HeaderProtection(hn, hp)
+    while time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        if ref is not None:
+            wire = [hpo.apply(p[:11], aead.encrypt(p[11:], p[:11], pn)) for p, pn in zip(pk, pns)]
+        else:
+            wire = [orc.protect(suite, key, iv, hp, p[:11], p[11:], pn) for p, pn in zip(pk, pns)]
+        t1 = time.perf_counter()
+        if ref is not None:
+            for x, pn in zip(wire, pns):
+                hdr, trunc = hpo.remove(x, 9)
+                pnd = decode_packet_number(trunc, ((hdr[0] & 3) + 1) * 8, pn)
+                aead.decrypt(x[len(hdr):], hdr, pnd)
+        else:
+            for x, pn in zip(wire, pns):
+                orc.unprotect(suite, key, iv, hp, x, 9, pn)
+        t2 = time.perf_counter()
+        t_p += t1 - t0
+        t_u += t2 - t1
+        done += m
+    value = done * 1200 / (t_p + t_u) / GIB
+    return {"value": round(value, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{done} packets of the bench workload ({cfg['name']}), suite {an.decode()}, "
+                      f"per-packet {'aioquic _crypto.c + OpenSSL' if kind == 'reference' else 'C oracle'}"
+                      f" calls, ~{seconds:.0f} s single thread"}
+
+
+# --------------------------------------------------------------------- main --
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import PacketEngine
+    from aioquic_amd.bench_data import make_workload
+
+    cfg = CONFIGS[args.config]
+    n = args.packets or cfg["n"]
+    # shard: rank r owns packets [r*n, (r+1)*n) of the global stream
+    w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=0x9001 + args.config,
+                      version=cfg["version"], mixed=cfg.get("mixed"), first_packet=rank * n)
+    eng = PacketEngine(w.n_keys)
+    eng.set_key_records(w.keys)
+
+    d_plain = torch.from_numpy(w.plain).to(dev)
+    d_desc = torch.from_numpy(w.desc.view(np.uint8)).to(dev)
+    d_udesc = torch.from_numpy(w.udesc.view(np.uint8)).to(dev)
+    d_wire = torch.zeros(w.wire_size, dtype=torch.uint8, device=dev)
+    d_back = torch.zeros(w.plain_size, dtype=torch.uint8, device=dev)
+    d_r1 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_r2 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        eng.protect(d_desc, n, d_plain, d_wire, d_r1, stream)
+        if ev:
+            ev[1].record(stream)
+        eng.unprotect(d_udesc, n, d_wire, d_back, d_r2, stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    t_prot = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
+    t_unp = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
+
+    ok = True
+    if args.check or True:
+        r1 = d_r1.cpu().numpy().view(L.RESULT)
+        r2 = d_r2.cpu().numpy().view(L.RESULT)
+        ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all())
+        if args.check:
+            ok = ok and bool(torch.equal(d_back.cpu(), d_plain.cpu()))
+
+    total_bytes = float(n) * 1200 * args.steps * world
+    value = total_bytes / elapsed / GIB
+    kern_t = max(t_prot, t_unp)
+    dom = "protect" if t_prot >= t_unp else "unprotect"
+    achieved = BYTES_PER_PKT_KERNEL * n / kern_t / 1e9
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if args.cpu_seconds > 0 and world == 1:
+            cpu = cpu_baseline(w, args.cpu_seconds, cfg)
+        out = {
+            "metric": "GiB/s device-resident AEAD protect+unprotect, 1200B packets",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded 1-RTT packets, 11 B header + 1173 B payload + 16 B tag)",
+            "config": {"workload": cfg["name"], "packets_per_gpu": n, "packet_bytes": 1200,
+                       "keys": w.n_keys, "parallelism": f"packet shards x{world}"},
+            "kernels_ms": {"protect": round(t_prot * 1e3, 4), "unprotect": round(t_unp * 1e3, 4)},
+            "kernel_gib_s": round(n * 1200 / (t_prot + t_unp) / GIB, 3),
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+            "cpu_baseline": cpu,
+            "status_ok": ok,
+        }
+        if args.e2e:
+            out["e2e"] = e2e(eng, w, dev, n)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def e2e(eng, w, dev, n, chunks=8, reps=5):
+    """Pinned host -> H2D -> protect -> unprotect -> D2H, pipelined over two
+    streams in `chunks` slices (the path starts and ends in UDP socket buffers)."""
+    import torch
+
+    h_in = torch.from_numpy(w.plain).pin_memory()
+    h_out = torch.empty_like(h_in).pin_memory()
+    d_in = torch.empty(w.plain_size, dtype=torch.uint8, device=dev)
+    d_wire = torch.empty(w.wire_size, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(w.plain_size, dtype=torch.uint8, device=dev)
+    per = n // chunks
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    descs, udescs, res = [], [], []
+    for c in range(chunks):
+        d = w.desc[c * per : (c + 1) * per].copy()
+        u = w.udesc[c * per : (c + 1) * per].copy()
+        descs.append(torch.from_numpy(d.view(np.uint8)).to(dev))
+        udescs.append(torch.from_numpy(u.view(np.uint8)).to(dev))
+        res.append(torch.empty(per * 16, dtype=torch.uint8, device=dev))
+    span = per * 1200
+    times = []
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for c in range(chunks):
+            s = streams[c % 2]
+            with torch.cuda.stream(s):
+                lo, hi = c * span, (c + 1) * span
+                d_in[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
+                eng.protect(descs[c], per, d_in, d_wire, res[c], s)
+                eng.unprotect(udescs[c], per, d_wire, d_out, res[c], s)
+                h_out[lo:hi].copy_(d_out[lo:hi], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"gib_s": round(per * chunks * 1200 / t / GIB, 3), "chunks": chunks,
+            "note": "pinned H2D + protect + unprotect + D2H, 2 streams"}
+
+
+if __name__ == "__main__":
+    main()

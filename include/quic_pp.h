@@ -33,7 +33,7 @@ extern "C" {
 
 #define QPP_PACKET_MAX 1500      /* _crypto.c:13 PACKET_LENGTH_MAX */
 #define QPP_TAG_LEN 16           /* _crypto.c:11 AEAD_TAG_LENGTH */
-#define QPP_MAX_HDR 255          /* longest header / associated data the kernels accept */
+#define QPP_MAX_HDR 1500         /* longest header / associated data the kernels accept */
 
 /* return codes of the API calls */
 #define QPP_OK 0
@@ -53,6 +53,10 @@ extern "C" {
 /* descriptor flags */
 #define QPP_F_NO_HP 1u      /* AEAD only (AEAD.encrypt/.decrypt): no header protection, no
                                packet-number decode, no key-phase check; hdr_len = AAD length */
+#define QPP_F_RFC_PN 2u     /* decode a 4-byte truncated packet number as unsigned (RFC 9000
+                               App. A.3).  Default: bit-exact with the reference, which hands
+                               the truncated number to Python as a signed int (_crypto.c:349),
+                               so values >= 2^31 decode differently once pn >= 2^32. */
 
 /* One packet of a batch.  Offsets are byte offsets into the caller's device
  * buffers; no alignment is required. */

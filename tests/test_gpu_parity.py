@@ -1,0 +1,391 @@
+"""GPU parity: the HIP path against the reference's golden vectors and the CPU
+oracle, through the C ABI (libquicpp via aioquic_amd._crypto).  Bit-exact."""
+
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from tests.golden_cases import gen_bytes, short_header
+
+pytestmark = pytest.mark.gpu
+
+SUITES = (0, 1, 2)
+KEY_LEN = {0: 16, 1: 32, 2: 32}
+
+
+@pytest.fixture(scope="module")
+def L():
+    from aioquic_amd import layout
+
+    return layout
+
+
+@pytest.fixture(scope="module")
+def engine_cls():
+    from aioquic_amd.batch import PacketEngine
+
+    return PacketEngine
+
+
+def _keys(rng, n_slots, suites=SUITES):
+    from aioquic_amd import layout as L
+
+    recs = np.zeros(n_slots, dtype=L.KEY_MATERIAL)
+    for s in range(n_slots):
+        suite = suites[s % len(suites)]
+        kl = KEY_LEN[suite]
+        recs[s]["slot"] = s
+        recs[s]["suite"] = suite
+        recs[s]["iv"] = np.frombuffer(rng.bytes(12), np.uint8)
+        recs[s]["key"][:kl] = np.frombuffer(rng.bytes(kl), np.uint8)
+        recs[s]["hp"][:kl] = np.frombuffer(rng.bytes(kl), np.uint8)
+    return recs
+
+
+def test_golden_vectors_batch(oracle, L, engine_cls):
+    """All reference golden cases in one protect batch and one unprotect batch."""
+    from tests.golden_util import case_inputs, load_cases, matches, tamper
+
+    cases = load_cases()
+    n = len(cases)
+    eng = engine_cls(2 * n)
+    recs = np.zeros(2 * n, dtype=L.KEY_MATERIAL)
+    xs = []
+    for i, c in enumerate(cases):
+        x = case_inputs(c, oracle)
+        xs.append(x)
+        kl = len(x["key"])
+        for slot, (k, iv, ph) in ((2 * i, (x["key"], x["iv"], 0)),
+                                  (2 * i + 1, (x["next_key"], x["next_iv"], 1))):
+            recs[slot]["slot"] = slot
+            recs[slot]["suite"] = c["suite"]
+            recs[slot]["key_phase"] = ph
+            recs[slot]["iv"] = np.frombuffer(iv, np.uint8)
+            recs[slot]["key"][:kl] = np.frombuffer(k, np.uint8)
+            recs[slot]["hp"][:kl] = np.frombuffer(x["hp"], np.uint8)
+    eng.set_key_records(recs)
+
+    from aioquic_amd.batch import layout_packets
+
+    inbuf, desc, size = layout_packets(
+        [x["header"] for x in xs], [x["payload"] for x in xs], [c["pn"] for c in cases],
+        [2 * i + c["send_phase"] for i, c in enumerate(cases)], align=1)
+    out, res = eng.protect_host(desc, inbuf.tobytes(), size)
+    assert (res["status"] == L.S_OK).all()
+    wires = []
+    for i, c in enumerate(cases):
+        o, ln = int(desc[i]["out_off"]), int(res[i]["out_len"])
+        pkt = out[o : o + ln].tobytes()
+        assert matches(c["protected"], pkt), c["seed"]
+        wires.append(tamper(c, pkt))
+
+    # unprotect: slot = receiver's current key (phase 0); KEY_PHASE -> retry with next
+    ud = np.zeros(n, dtype=L.DESC)
+    blob, pos = bytearray(), 0
+    for i, (c, w) in enumerate(zip(cases, wires)):
+        ud[i]["in_off"] = pos
+        ud[i]["out_off"] = pos
+        ud[i]["len"] = len(w)
+        ud[i]["hdr_len"] = c["pn_off"]
+        ud[i]["pn"] = c["expected_pn"]
+        ud[i]["slot"] = 2 * i
+        blob += w
+        pos += len(w)
+    out, res = eng.unprotect_host(ud, bytes(blob), pos)
+    retry = np.nonzero(res["status"] == L.S_KEY_PHASE)[0]
+    res = res.copy()
+    out = out.copy()
+    if len(retry):
+        ud2 = ud[retry].copy()
+        ud2["slot"] += 1
+        out2, res2 = eng.unprotect_host(ud2, bytes(blob), pos)
+        for j, i in enumerate(retry):
+            res[i] = res2[j]
+            o = int(ud[i]["out_off"])
+            out[o : o + int(res2[j]["out_len"])] = out2[o : o + int(res2[j]["out_len"])]
+    for i, c in enumerate(cases):
+        exp = c["unprotect"]
+        st = int(res[i]["status"])
+        if not exp["ok"]:
+            assert st == L.S_DECRYPT, (c["seed"], st)
+            continue
+        assert st == L.S_OK, (c["seed"], st)
+        assert (i in retry) == exp["phase_flip"]
+        o, hl, ln = int(ud[i]["out_off"]), int(res[i]["hdr_len"]), int(res[i]["out_len"])
+        assert out[o : o + hl].tobytes().hex() == exp["header"], c["seed"]
+        assert matches(exp["payload"], out[o + hl : o + ln].tobytes()), c["seed"]
+        assert int(res[i]["pn"]) == exp["pn"], c["seed"]
+
+
+def _random_batch(rng, n, n_slots, recs, *, max_payload=1400, pn_lens=(1, 2, 3, 4)):
+    headers, payloads, pns, slots = [], [], [], []
+    for i in range(n):
+        pn_len = pn_lens[i % len(pn_lens)]
+        pn = int(rng.integers(0, 1 << 40))
+        if i % 5 == 4:
+            dcid = rng.bytes(int(rng.integers(0, 21)))
+            token = rng.bytes(int(rng.integers(0, 60)))
+            hdr = (bytes([0xC0 | (pn_len - 1)]) + (1).to_bytes(4, "big") + bytes([len(dcid)]) +
+                   dcid + b"\x00" + bytes([len(token)]) + token + b"\x44\x00" +
+                   (pn & ((1 << (8 * pn_len)) - 1)).to_bytes(pn_len, "big"))
+        else:
+            hdr = short_header(rng.bytes(int(rng.integers(0, 21))), pn, pn_len, 0, spin=i & 1)
+        plen = int(rng.integers(max(0, 4 - pn_len), max_payload))
+        plen = min(plen, 1500 - 16 - len(hdr))
+        headers.append(hdr)
+        payloads.append(rng.bytes(plen))
+        pns.append(pn)
+        slots.append(int(rng.integers(0, n_slots)))
+    return headers, payloads, pns, slots
+
+
+@pytest.mark.parametrize("align", [1, 16])
+def test_random_batch_vs_oracle(oracle, L, engine_cls, align):
+    """Ragged, misaligned packets of all suites and mixed key slots vs the oracle."""
+    from aioquic_amd.batch import layout_packets
+
+    rng = np.random.default_rng(0x9001 + align)
+    n_slots = 24
+    recs = _keys(rng, n_slots)
+    eng = engine_cls(n_slots)
+    eng.set_key_records(recs)
+    headers, payloads, pns, slots = _random_batch(rng, 3000, n_slots, recs)
+    inbuf, desc, size = layout_packets(headers, payloads, pns, slots, align=align)
+    out_g, res_g = eng.protect_host(desc, inbuf.tobytes(), size)
+    out_o, res_o = oracle.protect_batch(recs, desc, inbuf, size)
+    assert (res_g["status"] == res_o["status"]).all()
+    assert (res_g["out_len"] == res_o["out_len"]).all()
+    assert np.array_equal(out_g, out_o)
+
+    # unprotect what the GPU produced, with expected pn = pn (+ jitter)
+    ud = desc.copy()
+    ud["len"] = res_g["out_len"]
+    ud["hdr_len"] = [len(h) - ((h[0] & 3) + 1) for h in headers]
+    ud["pn"] = np.asarray(pns, np.uint64) + rng.integers(0, 50, size=len(pns)).astype(np.uint64)
+    u_g, r_g = eng.unprotect_host(ud, out_g.tobytes(), size)
+    u_o, r_o = oracle.unprotect_batch(recs, ud, out_g, size)
+    assert (r_g["status"] == L.S_OK).all()
+    assert (r_g == r_o).all()
+    assert np.array_equal(u_g, u_o)
+    # round trip restores the input (header + payload)
+    for i in range(len(headers)):
+        o = int(desc[i]["in_off"])
+        n_ = len(headers[i]) + len(payloads[i])
+        assert u_g[o : o + n_].tobytes() == headers[i] + payloads[i]
+
+
+def test_tamper_and_edge_status(oracle, L, engine_cls):
+    """Corrupted tags/ciphertext -> DECRYPT for exactly those packets; bad
+    lengths -> LENGTH; empty slot -> NO_KEY; key phase flip -> KEY_PHASE."""
+    from aioquic_amd.batch import layout_packets
+
+    rng = np.random.default_rng(7)
+    recs = _keys(rng, 6)
+    eng = engine_cls(8)
+    eng.set_key_records(recs)
+    n = 600
+    headers = [short_header(rng.bytes(8), i, 2, 0) for i in range(n)]
+    payloads = [rng.bytes(int(rng.integers(4, 1200))) for _ in range(n)]
+    slots = [i % 6 for i in range(n)]
+    inbuf, desc, size = layout_packets(headers, payloads, list(range(n)), slots)
+    out, res = eng.protect_host(desc, inbuf.tobytes(), size)
+    assert (res["status"] == L.S_OK).all()
+    wire = out.copy()
+    bad = set(int(i) for i in rng.choice(n, 60, replace=False))
+    for i in bad:
+        o = int(desc[i]["out_off"]) + 11 + int(rng.integers(0, len(payloads[i]) + 16))
+        wire[o] ^= 1 << int(rng.integers(0, 8))
+    ud = desc.copy()
+    ud["len"] = res["out_len"]
+    ud["hdr_len"] = 9
+    ud[3]["len"] = 25          # too short for header + tag
+    ud[5]["slot"] = 7          # never installed
+    ud[7]["hdr_len"] = 0       # pn offset 0
+    u, r = eng.unprotect_host(ud, wire.tobytes(), size)
+    uo, ro = oracle.unprotect_batch(recs, ud, wire, size)
+    for i in range(n):
+        st = int(r[i]["status"])
+        if i == 5:
+            assert st == L.S_NO_KEY
+        elif i in (3, 7):
+            assert st == L.S_LENGTH
+        elif i in bad:
+            assert st == L.S_DECRYPT, i
+        else:
+            assert st == L.S_OK, i
+        if i not in (5,):
+            assert st == int(ro[i]["status"]), i
+    # key-phase: flip the receiver's phase for slot 0
+    recs2 = recs.copy()
+    recs2[0]["key_phase"] = 1
+    eng.set_key_records(recs2[:1])
+    u, r = eng.unprotect_host(ud, wire.tobytes(), size)
+    for i in range(0, n, 6):
+        if i not in bad and i not in (3, 5, 7):
+            assert int(r[i]["status"]) == L.S_KEY_PHASE
+
+
+def test_aead_only_batch(oracle, L, engine_cls):
+    """QPP_F_NO_HP: AEAD.encrypt / AEAD.decrypt semantics, arbitrary AAD incl. empty."""
+    from aioquic_amd.batch import layout_packets
+
+    rng = np.random.default_rng(11)
+    recs = _keys(rng, 3)
+    eng = engine_cls(3)
+    eng.set_key_records(recs)
+    aads = [rng.bytes(int(rng.integers(0, 70))) for _ in range(400)]
+    datas = [rng.bytes(int(rng.integers(0, 1500))) for _ in range(400)]
+    pns = [int(rng.integers(0, 1 << 63)) for _ in range(400)]
+    inbuf, desc, size = layout_packets(aads, datas, pns, [i % 3 for i in range(400)],
+                                       flags=L.F_NO_HP)
+    out, res = eng.protect_host(desc, inbuf.tobytes(), size)
+    out_o, res_o = oracle.protect_batch(recs, desc, inbuf, size)
+    assert (res["status"] == 0).all() and (res == res_o).all()
+    assert np.array_equal(out, out_o)
+    ud = desc.copy()
+    ud["len"] = res["out_len"]
+    u, r = eng.unprotect_host(ud, out.tobytes(), size)
+    uo, ro = oracle.unprotect_batch(recs, ud, out, size)
+    assert (r["status"] == 0).all() and (r == ro).all()
+    assert np.array_equal(u, uo)
+
+
+def test_full_size_round_trip_64k(L, engine_cls):
+    """BASELINE config 2 shape on device tensors: 64Ki x 1200 B, AES-128-GCM,
+    one key.  Size-independent properties: round trip identity, all tags
+    verify, every ciphertext differs from its plaintext, and a checksum of the
+    protected batch against the oracle on a sampled subset."""
+    import torch
+
+    from aioquic_amd import bench_data
+
+    n = 65536
+    w = bench_data.make_workload(n, suite=0, n_keys=1, seed=0x9002)
+    eng = engine_cls(w.n_keys)
+    eng.set_key_records(w.keys)
+    dev = torch.device("cuda")
+    d_in = torch.from_numpy(w.plain).to(dev)
+    d_desc = torch.from_numpy(w.desc.view(np.uint8)).to(dev)
+    d_wire = torch.empty(w.wire_size, dtype=torch.uint8, device=dev)
+    d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    eng.protect(d_desc, n, d_in, d_wire, d_res)
+    d_udesc = torch.from_numpy(w.udesc.view(np.uint8)).to(dev)
+    d_back = torch.zeros(w.plain_size, dtype=torch.uint8, device=dev)
+    d_res2 = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    eng.unprotect(d_udesc, n, d_wire, d_back, d_res2)
+    torch.cuda.synchronize()
+    r1 = d_res.cpu().numpy().view(L.RESULT)
+    r2 = d_res2.cpu().numpy().view(L.RESULT)
+    assert (r1["status"] == 0).all() and (r1["out_len"] == 1200).all()
+    assert (r2["status"] == 0).all() and (r2["pn"] == w.desc["pn"]).all()
+    back = d_back.cpu().numpy()
+    assert np.array_equal(back, w.plain)
+    wire = d_wire.cpu().numpy()
+    # sampled oracle parity
+    from oracle import oracle as orc
+
+    idx = np.random.default_rng(3).choice(n, 256, replace=False)
+    sub = w.desc[idx].copy()
+    o_out, o_res = orc.protect_batch(w.keys, sub, w.plain, w.wire_size)
+    for j, i in enumerate(idx):
+        o = int(w.desc[i]["out_off"])
+        assert np.array_equal(o_out[o : o + 1200], wire[o : o + 1200])
+    assert hashlib.sha256(wire.tobytes()).hexdigest() != hashlib.sha256(back.tobytes()).hexdigest()
+
+
+def test_object_api():
+    """aioquic._crypto object semantics (errors, signed pn from remove)."""
+    from aioquic_amd._crypto import AEAD, CryptoError, HeaderProtection
+
+    with pytest.raises(CryptoError, match="Invalid cipher name: foo"):
+        AEAD(b"foo", bytes(16), bytes(12))
+    with pytest.raises(CryptoError, match="Invalid key length"):
+        AEAD(b"aes-128-gcm", bytes(33), bytes(12))
+    with pytest.raises(CryptoError, match="Invalid iv length"):
+        AEAD(b"aes-128-gcm", bytes(16), bytes(13))
+    with pytest.raises(CryptoError, match="OpenSSL call failed"):
+        AEAD(b"aes-128-gcm", bytes(32), bytes(12))
+    a = AEAD(b"aes-128-gcm", bytes(16), bytes(12))
+    with pytest.raises(CryptoError, match="Invalid payload length"):
+        a.decrypt(b"x" * 15, b"", 0)
+    with pytest.raises(CryptoError, match="Invalid payload length"):
+        a.encrypt(b"x" * 1501, b"", 0)
+    with pytest.raises(CryptoError, match="Payload decryption failed"):
+        a.decrypt(b"x" * 16, b"", 0)
+    ct = a.encrypt(b"hello", b"hdr", 5)
+    assert a.decrypt(ct, b"hdr", 5) == b"hello"
+    # short iv is zero padded (reference: memcpy into a zeroed object)
+    assert AEAD(b"aes-128-gcm", bytes(16), bytes(8)).encrypt(b"abc", b"", 0) == \
+        a.encrypt(b"abc", b"", 0)
+    with pytest.raises(CryptoError, match="OpenSSL call failed"):
+        HeaderProtection(b"aes-128-ecb", bytes(32))
+    hp = HeaderProtection(b"aes-128-ecb", bytes(16))
+    # known value from the reference build (aes-128-ecb of zeros under key 0)
+    hdr, pn = hp.remove(bytes(30), 5)
+    assert hdr.hex() == "0600000000e94bd4" and pn == 15289300
+
+
+def test_object_api_vs_oracle(oracle):
+    from aioquic_amd._crypto import AEAD, HeaderProtection
+
+    rng = np.random.default_rng(5)
+    names = {0: (b"aes-128-gcm", b"aes-128-ecb"), 1: (b"aes-256-gcm", b"aes-256-ecb"),
+             2: (b"chacha20-poly1305", b"chacha20")}
+    for suite in SUITES:
+        kl = KEY_LEN[suite]
+        key, iv, hpk = rng.bytes(kl), rng.bytes(12), rng.bytes(kl)
+        a = AEAD(names[suite][0], key, iv)
+        h = HeaderProtection(names[suite][1], hpk)
+        for ln in (0, 1, 15, 16, 17, 100, 1484, 1500):
+            data, aad, pn = rng.bytes(ln), rng.bytes(int(rng.integers(0, 40))), int(rng.integers(0, 1 << 62))
+            ct = a.encrypt(data, aad, pn)
+            assert ct == oracle.aead_encrypt(suite, key, iv, data, aad, pn)
+            assert a.decrypt(ct, aad, pn) == data
+        for _ in range(10):
+            sample = rng.bytes(16)
+            pkt = rng.bytes(5) + sample + rng.bytes(3)
+            hdr, pn = h.remove(pkt, 1)
+            m = oracle.hp_mask(suite, hpk, sample)
+            b0 = pkt[0] ^ (m[0] & (0x0F if pkt[0] & 0x80 else 0x1F))
+            pl = (b0 & 3) + 1
+            assert hdr[0] == b0 and len(hdr) == 1 + pl
+            t = int.from_bytes(bytes(x ^ y for x, y in zip(pkt[1 : 1 + pl], m[1 : 1 + pl])), "big")
+            assert pn == (t - (1 << 32) if t >= 1 << 31 else t)
+
+
+def test_retry_integrity_tag():
+    """Retry tags of RFC 9001 / RFC 9369 App. A.4 (reference tests/test_packet.py:111-189)."""
+    from aioquic_amd.packet import QuicProtocolVersion, get_retry_integrity_tag
+
+    odcid = bytes.fromhex("8394c8f03e515708")
+    v1 = bytes.fromhex("ff000000010008f067a5502a4262b5746f6b656e04a265ba2eff4d829058fb3f0f2496ba")
+    v2 = bytes.fromhex("cf6b3343cf0008f067a5502a4262b5746f6b656ec8646ce8bfe33952d955543665dcc7b6")
+    assert get_retry_integrity_tag(v1[:20], odcid, QuicProtocolVersion.VERSION_1) == v1[20:]
+    assert get_retry_integrity_tag(v2[:20], odcid, QuicProtocolVersion.VERSION_2) == v2[20:]
+
+
+def test_in_place(oracle, L, engine_cls):
+    """out buffer == in buffer (the builder encrypts in place, packet_builder.py:341-350)."""
+    import torch
+
+    from aioquic_amd.batch import layout_packets
+
+    rng = np.random.default_rng(9)
+    recs = _keys(rng, 3)
+    eng = engine_cls(3)
+    eng.set_key_records(recs)
+    headers = [short_header(rng.bytes(8), i, 2, 0) for i in range(256)]
+    payloads = [rng.bytes(int(rng.integers(4, 1300))) for _ in range(256)]
+    inbuf, desc, size = layout_packets(headers, payloads, list(range(256)), [i % 3 for i in range(256)])
+    exp, _ = oracle.protect_batch(recs, desc, inbuf, size)
+    buf = torch.from_numpy(inbuf.copy()).cuda()
+    d = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
+    res = torch.empty(256 * 16, dtype=torch.uint8, device="cuda")
+    eng.protect(d, 256, buf, buf, res)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    for i in range(256):
+        o, n = int(desc[i]["out_off"]), len(headers[i]) + len(payloads[i]) + 16
+        assert np.array_equal(got[o : o + n], exp[o : o + n])
