@@ -820,6 +820,8 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
     if (in_len) memcpy(s->h_in, in, in_len);
     HIPCHK(hipMemcpyAsync(dd, hd, (size_t)n * sizeof(qpp_desc), hipMemcpyHostToDevice, s->stream));
     if (in_len) HIPCHK(hipMemcpyAsync(s->d_in, s->h_in, in_len, hipMemcpyHostToDevice, s->stream));
+    // bytes the kernel does not write (gaps, failed packets) come back as zeros
+    if (out_len) HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     rc = launch_packets(enc, kt, dd, n, s->d_in, s->d_out, dr, s->stream);
     if (rc != QPP_OK) return rc;
     if (out_len) HIPCHK(hipMemcpyAsync(s->h_out, s->d_out, out_len, hipMemcpyDeviceToHost, s->stream));

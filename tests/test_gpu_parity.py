@@ -166,14 +166,21 @@ def test_random_batch_vs_oracle(oracle, L, engine_cls, align):
     ud["pn"] = np.asarray(pns, np.uint64) + rng.integers(0, 50, size=len(pns)).astype(np.uint64)
     u_g, r_g = eng.unprotect_host(ud, out_g.tobytes(), size)
     u_o, r_o = oracle.unprotect_batch(recs, ud, out_g, size)
-    assert (r_g["status"] == L.S_OK).all()
-    assert (r_g == r_o).all()
-    assert np.array_equal(u_g, u_o)
-    # round trip restores the input (header + payload)
+    bad = np.nonzero(r_g != r_o)[0]
+    assert len(bad) == 0, (bad[:10], r_g[bad[:3]], r_o[bad[:3]])
+    # the only failures allowed are the reference's signed-pn quirk: 4-byte
+    # packet number >= 2^32 whose truncated value has its top bit set
+    quirk = np.array([((h[0] & 3) == 3) and pn >= (1 << 32) and (pn & 0x80000000) != 0
+                      for h, pn in zip(headers, pns)])
+    assert ((r_g["status"] == L.S_OK) | quirk).all()
+    assert ((r_g["status"] == L.S_DECRYPT) == quirk).all()
+    # round trip restores the input (header + payload); outputs equal the oracle's
     for i in range(len(headers)):
         o = int(desc[i]["in_off"])
         n_ = len(headers[i]) + len(payloads[i])
-        assert u_g[o : o + n_].tobytes() == headers[i] + payloads[i]
+        if not quirk[i]:
+            assert u_g[o : o + n_].tobytes() == headers[i] + payloads[i]
+            assert np.array_equal(u_g[o : o + n_], u_o[o : o + n_])
 
 
 def test_tamper_and_edge_status(oracle, L, engine_cls):
@@ -212,11 +219,14 @@ def test_tamper_and_edge_status(oracle, L, engine_cls):
         elif i in (3, 7):
             assert st == L.S_LENGTH
         elif i in bad:
-            assert st == L.S_DECRYPT, i
+            # a flipped sample bit changes the unmasked first byte, which can
+            # flip the key-phase bit or the pn length; the oracle agrees
+            assert st != L.S_OK, i
         else:
             assert st == L.S_OK, i
-        if i not in (5,):
-            assert st == int(ro[i]["status"]), i
+        assert st == int(ro[i]["status"]), i
+        if st == L.S_OK:
+            assert r[i] == ro[i]
     # key-phase: flip the receiver's phase for slot 0
     recs2 = recs.copy()
     recs2[0]["key_phase"] = 1
@@ -243,7 +253,13 @@ def test_aead_only_batch(oracle, L, engine_cls):
     out, res = eng.protect_host(desc, inbuf.tobytes(), size)
     out_o, res_o = oracle.protect_batch(recs, desc, inbuf, size)
     assert (res["status"] == 0).all() and (res == res_o).all()
-    assert np.array_equal(out, out_o)
+    diff = np.nonzero(out != out_o)[0]
+    if len(diff):
+        starts = desc["out_off"].astype(np.int64)
+        k = int(np.searchsorted(starts, diff[0], side="right") - 1)
+        raise AssertionError(f"first diff at byte {diff[0]} ({len(diff)} total) in packet {k}: "
+                             f"aad {len(aads[k])} data {len(datas[k])} slot {k % 3} "
+                             f"suite {recs[k % 3]['suite']} off {diff[0] - starts[k]}")
     ud = desc.copy()
     ud["len"] = res["out_len"]
     u, r = eng.unprotect_host(ud, out.tobytes(), size)
@@ -328,7 +344,7 @@ def test_object_api():
 
 
 def test_object_api_vs_oracle(oracle):
-    from aioquic_amd._crypto import AEAD, HeaderProtection
+    from aioquic_amd._crypto import AEAD, CryptoError, HeaderProtection
 
     rng = np.random.default_rng(5)
     names = {0: (b"aes-128-gcm", b"aes-128-ecb"), 1: (b"aes-256-gcm", b"aes-256-ecb"),
@@ -342,7 +358,11 @@ def test_object_api_vs_oracle(oracle):
             data, aad, pn = rng.bytes(ln), rng.bytes(int(rng.integers(0, 40))), int(rng.integers(0, 1 << 62))
             ct = a.encrypt(data, aad, pn)
             assert ct == oracle.aead_encrypt(suite, key, iv, data, aad, pn)
-            assert a.decrypt(ct, aad, pn) == data
+            if len(ct) <= 1500:
+                assert a.decrypt(ct, aad, pn) == data
+            else:  # the reference rejects data (ct||tag) longer than 1500 bytes
+                with pytest.raises(CryptoError, match="Invalid payload length"):
+                    a.decrypt(ct, aad, pn)
         for _ in range(10):
             sample = rng.bytes(16)
             pkt = rng.bytes(5) + sample + rng.bytes(3)
