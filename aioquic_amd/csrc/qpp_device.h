@@ -160,43 +160,75 @@ __device__ __forceinline__ u32x4 quad_xor_all(u32x4 v)
 
 // ------------------------------------------------------------------- AES --
 
-// T-table lookups.  The LDS copy of Te0 is replicated 32 times so that lane l
-// always reads bank (l & 31): entry x of copy c lives at byte x*128 + c*4.
-// `lo` = (lane & 31) * 4.  For every byte position the address is one shift
-// and one and-or.
+// T-table lookups.  A lookup object provides, for byte r of a state word s,
+//   t<r>(s) = Te_r[byte r of s]  (Te_r = Te0 rotated left by 8r)
+// The LDS image holds Te0 and Te1, each replicated 32 times so lane l always
+// reads bank (l & 31): entry x occupies one 256-byte row,
+//   [Te0[x] copy 0..31][Te1[x] copy 0..31],
+// so the address of byte r of s is (byte_r(s) << 8) | (lane&31)*4 -- a single
+// v_perm -- with Te1 at immediate offset +128.  Te2 / Te3 are Te0 / Te1
+// rotated by 16.  64 KiB of LDS.
+constexpr int kTeBytes = 256 * 256;
+
 struct LdsTe {
-    const uint32_t *te;  // LDS base
-    uint32_t lo;
-    __device__ __forceinline__ uint32_t b0(uint32_t s) const
+    const uint8_t *te;  // LDS base of the 64 KiB image
+    uint32_t lo;        // (lane & 31) * 4
+    template <int R>
+    __device__ __forceinline__ uint32_t addr(uint32_t s) const
     {
-        return *(const uint32_t *)((const uint8_t *)te + (((s << 7) & 0x7f80u) | lo));
+        // bytes {S0=s, S1=lo}: result byte0 = lo.byte0, byte1 = s.byte R, bytes 2,3 = 0
+        return __builtin_amdgcn_perm(s, lo, 0x0c0c0000u | ((4u + R) << 8));
     }
-    __device__ __forceinline__ uint32_t b1(uint32_t s) const
+    __device__ __forceinline__ uint32_t t0(uint32_t s) const
     {
-        return *(const uint32_t *)((const uint8_t *)te + (((s >> 1) & 0x7f80u) | lo));
+        return *(const uint32_t *)(te + addr<0>(s));
     }
-    __device__ __forceinline__ uint32_t b2(uint32_t s) const
+    __device__ __forceinline__ uint32_t t1(uint32_t s) const
     {
-        return *(const uint32_t *)((const uint8_t *)te + (((s >> 9) & 0x7f80u) | lo));
+        return *(const uint32_t *)(te + 128 + addr<1>(s));
     }
-    __device__ __forceinline__ uint32_t b3(uint32_t s) const
+    __device__ __forceinline__ uint32_t t2(uint32_t s) const
     {
-        return *(const uint32_t *)((const uint8_t *)te + (((s >> 17) & 0x7f80u) | lo));
+        return rotl(*(const uint32_t *)(te + addr<2>(s)), 16);
+    }
+    __device__ __forceinline__ uint32_t t3(uint32_t s) const
+    {
+        return rotl(*(const uint32_t *)(te + 128 + addr<3>(s)), 16);
+    }
+    // final round: S(x) placed at byte r.  Te0 = (2S,S,S,3S), Te1 = (3S,2S,S,S)
+    __device__ __forceinline__ uint32_t f0(uint32_t s) const
+    {
+        return (*(const uint32_t *)(te + addr<0>(s)) >> 8) & 0xffu;
+    }
+    __device__ __forceinline__ uint32_t f1(uint32_t s) const
+    {
+        return *(const uint32_t *)(te + addr<1>(s)) & 0xff00u;
+    }
+    __device__ __forceinline__ uint32_t f2(uint32_t s) const
+    {
+        return *(const uint32_t *)(te + 128 + addr<2>(s)) & 0xff0000u;
+    }
+    __device__ __forceinline__ uint32_t f3(uint32_t s) const
+    {
+        return *(const uint32_t *)(te + 128 + addr<3>(s)) & 0xff000000u;
     }
 };
 
 // Constant-memory lookups (key setup and other cold paths).
 struct ConstTe {
-    __device__ __forceinline__ uint32_t b0(uint32_t s) const { return c_aes.te0[s & 255]; }
-    __device__ __forceinline__ uint32_t b1(uint32_t s) const { return c_aes.te0[(s >> 8) & 255]; }
-    __device__ __forceinline__ uint32_t b2(uint32_t s) const { return c_aes.te0[(s >> 16) & 255]; }
-    __device__ __forceinline__ uint32_t b3(uint32_t s) const { return c_aes.te0[s >> 24]; }
+    __device__ __forceinline__ uint32_t t0(uint32_t s) const { return c_aes.te0[s & 255]; }
+    __device__ __forceinline__ uint32_t t1(uint32_t s) const { return rotl(c_aes.te0[(s >> 8) & 255], 8); }
+    __device__ __forceinline__ uint32_t t2(uint32_t s) const { return rotl(c_aes.te0[(s >> 16) & 255], 16); }
+    __device__ __forceinline__ uint32_t t3(uint32_t s) const { return rotl(c_aes.te0[s >> 24], 24); }
+    __device__ __forceinline__ uint32_t f0(uint32_t s) const { return c_aes.sbox[s & 255]; }
+    __device__ __forceinline__ uint32_t f1(uint32_t s) const { return (uint32_t)c_aes.sbox[(s >> 8) & 255] << 8; }
+    __device__ __forceinline__ uint32_t f2(uint32_t s) const { return (uint32_t)c_aes.sbox[(s >> 16) & 255] << 16; }
+    __device__ __forceinline__ uint32_t f3(uint32_t s) const { return (uint32_t)c_aes.sbox[s >> 24] << 24; }
 };
 
 // One AES encryption, state and round keys as little-endian column words.
-// Round: column c takes row r from column c+r (ShiftRows) through Te0 rotated
-// left by 8r (MixColumns coefficients).  Final round keeps S(x), found in
-// bytes 1 and 2 of Te0[x].
+// Round: column c takes row r from column c+r (ShiftRows) through Te_r
+// (MixColumns coefficients); the final round substitutes only.
 template <int NR, class TE>
 __device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, const TE &T)
 {
@@ -204,23 +236,17 @@ __device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, const
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
-        uint32_t t0 = xor3(xor3(T.b0(s0), rotl(T.b1(s1), 8), rotl(T.b2(s2), 16)),
-                           rotl(T.b3(s3), 24), k[0]);
-        uint32_t t1 = xor3(xor3(T.b0(s1), rotl(T.b1(s2), 8), rotl(T.b2(s3), 16)),
-                           rotl(T.b3(s0), 24), k[1]);
-        uint32_t t2 = xor3(xor3(T.b0(s2), rotl(T.b1(s3), 8), rotl(T.b2(s0), 16)),
-                           rotl(T.b3(s1), 24), k[2]);
-        uint32_t t3 = xor3(xor3(T.b0(s3), rotl(T.b1(s0), 8), rotl(T.b2(s1), 16)),
-                           rotl(T.b3(s2), 24), k[3]);
+        uint32_t t0 = xor3(xor3(T.t0(s0), T.t1(s1), T.t2(s2)), T.t3(s3), k[0]);
+        uint32_t t1 = xor3(xor3(T.t0(s1), T.t1(s2), T.t2(s3)), T.t3(s0), k[1]);
+        uint32_t t2 = xor3(xor3(T.t0(s2), T.t1(s3), T.t2(s0)), T.t3(s1), k[2]);
+        uint32_t t3 = xor3(xor3(T.t0(s3), T.t1(s0), T.t2(s1)), T.t3(s2), k[3]);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint32_t *k = rk + 4 * NR;
-    auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t key) {
-        return (((T.b0(a) >> 8) & 0xffu) | (T.b1(b) & 0xff00u) | (T.b2(c) & 0xff0000u) |
-                ((T.b3(d) << 8) & 0xff000000u)) ^ key;
-    };
-    return u32x4{fin(s0, s1, s2, s3, k[0]), fin(s1, s2, s3, s0, k[1]),
-                 fin(s2, s3, s0, s1, k[2]), fin(s3, s0, s1, s2, k[3])};
+    return u32x4{(T.f0(s0) | T.f1(s1) | T.f2(s2) | T.f3(s3)) ^ k[0],
+                 (T.f0(s1) | T.f1(s2) | T.f2(s3) | T.f3(s0)) ^ k[1],
+                 (T.f0(s2) | T.f1(s3) | T.f2(s0) | T.f3(s1)) ^ k[2],
+                 (T.f0(s3) | T.f1(s0) | T.f2(s1) | T.f3(s2)) ^ k[3]};
 }
 
 // --------------------------------------------------------------- GHASH ----

@@ -27,23 +27,29 @@ namespace qpp {
 
 __constant__ AesTables c_aes = kAesTables;
 
-constexpr int kWG = 256;
+// One 1024-thread workgroup per CU: 16 waves (4 per SIMD, so <= 128 VGPRs)
+// share one 64 KiB AES image and one 32 KiB GHASH table set.
+constexpr int kWG = 1024;
 constexpr int kPktPerWG = kWG / 4;
 constexpr int kScratch = 48;  // (ct||tag)[0..48) per packet, for the HP sample
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
 struct __attribute__((aligned(16))) Smem {
-    uint32_t te[256 * 32];            // Te0 x 32 bank copies   32 KiB
-    uint8_t gt[kGhashTabBytes];       // GHASH H^1..H^4 tables   32 KiB
+    uint8_t te[kTeBytes];             // Te0|Te1 x 32 bank copies   64 KiB
+    uint8_t gt[kGhashTabBytes];       // GHASH H^1..H^4 tables      32 KiB
     uint8_t scratch[kPktPerWG][kScratch];
     uint32_t cur_slot;
 };
 
-__device__ __forceinline__ void load_te(Smem &sm)
+// Fill the LDS AES image: row x = [Te0[x] x 32 | Te1[x] x 32], 16-byte stores.
+template <int NT>
+__device__ __forceinline__ void load_te(uint8_t *te)
 {
-    for (int i = threadIdx.x; i < 256 * 8; i += kWG) {
-        uint32_t v = c_aes.te0[i >> 3];
-        *(u32x4 *)&sm.te[(i >> 3) * 32 + (i & 7) * 4] = u32x4{v, v, v, v};
+    for (int i = threadIdx.x; i < 256 * 16; i += NT) {
+        const int x = i >> 4, part = i & 15;
+        const uint32_t v0 = c_aes.te0[x];
+        const uint32_t v = part < 8 ? v0 : rotl(v0, 8);
+        *(u32x4 *)(te + x * 256 + part * 16) = u32x4{v, v, v, v};
     }
 }
 
@@ -95,17 +101,27 @@ __device__ __forceinline__ u32x4 lds_sample(const uint8_t *scr, int s)
                  __builtin_amdgcn_alignbyte(d, c, s), __builtin_amdgcn_alignbyte(e, d, s)};
 }
 
-template <class TE>
-__device__ __forceinline__ u32x4 hp_mask_of(const KeySlot *ks, uint32_t suite, u32x4 sample,
-                                            const TE &T)
+// HeaderProtection_mask (_crypto.c:278-287): AES-ECB(hp, sample), or the
+// first ChaCha20 block with counter = sample[0:4] and nonce = sample[4:16].
+template <int SUITE, class TE>
+__device__ __forceinline__ u32x4 hp_mask_of(const KeySlot *ks, u32x4 sample, const TE &T)
 {
-    if (suite == QPP_CHACHA20_POLY1305) {
+    if constexpr (SUITE == QPP_CHACHA20_POLY1305) {
         uint32_t blk[16];
         chacha_block(ks->hrk, sample.x, sample.y, sample.z, sample.w, blk);
         return u32x4{blk[0], blk[1], blk[2], blk[3]};
+    } else {
+        return aes_encrypt<SUITE == QPP_AES_256_GCM ? 14 : 10>(sample, ks->hrk, T);
     }
-    if (suite == QPP_AES_256_GCM) return aes_encrypt<14>(sample, ks->hrk, T);
-    return aes_encrypt<10>(sample, ks->hrk, T);
+}
+
+template <class TE>
+__device__ __forceinline__ u32x4 hp_mask_any(const KeySlot *ks, uint32_t suite, u32x4 sample,
+                                             const TE &T)
+{
+    if (suite == QPP_CHACHA20_POLY1305) return hp_mask_of<QPP_CHACHA20_POLY1305>(ks, sample, T);
+    if (suite == QPP_AES_256_GCM) return hp_mask_of<QPP_AES_256_GCM>(ks, sample, T);
+    return hp_mask_of<QPP_AES_128_GCM>(ks, sample, T);
 }
 
 // -------------------------------------------------------- per-packet view --
@@ -125,9 +141,9 @@ struct Pkt {
 
 // Header analysis shared by both suites.  Unprotect removes header
 // protection here (it decides the header length and the packet number).
-template <bool ENC, class TE>
+template <bool ENC, int SUITE, class TE>
 __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const uint8_t *gin, uint8_t *gout,
-                                         const KeySlot *ks, uint32_t suite, const TE &T)
+                                         const KeySlot *ks, const TE &T)
 {
     Pkt P;
     P.src = gin + d.in_off;
@@ -165,7 +181,7 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const uint8_t *gin, 
             P.status = QPP_S_LENGTH;
         } else {
             const u32x4 sample = ld16(P.src + P.pn_off + 4);
-            P.mask = hp_mask_of(ks, suite, sample, T);
+            P.mask = hp_mask_of<SUITE>(ks, sample, T);
             uint32_t b0 = P.src[0];
             P.fbm = first_byte_mask(b0);
             b0 ^= byte_of(P.mask, 0) & P.fbm;
@@ -196,9 +212,9 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const uint8_t *gin, 
 }
 
 // Protect: header protection over the finished (ct||tag) and the header write.
-template <class TE>
-__device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, uint32_t suite,
-                                                  int sub, uint8_t *scr, u32x4 tag, const TE &T)
+template <int SUITE, class TE>
+__device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int sub,
+                                                  uint8_t *scr, u32x4 tag, const TE &T)
 {
     // sample = (ct||tag)[4-pn_len : 20-pn_len]; the tag only matters when clen < 20
     if (P.clen < 32 && sub == 0) {
@@ -207,7 +223,7 @@ __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, uin
     }
     __builtin_amdgcn_wave_barrier();
     const u32x4 sample = lds_sample(scr, 4 - P.pn_len);
-    P.mask = hp_mask_of(ks, suite, sample, T);
+    P.mask = hp_mask_of<SUITE>(ks, sample, T);
     const int n_a = (P.hlen + 15) >> 4;
     for (int q = sub; q < n_a; q += 4) {
         const int nb = min(16, P.hlen - 16 * q);
@@ -219,9 +235,9 @@ __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, uin
 
 // --------------------------------------------------------------- AES-GCM --
 
-template <int NR, bool ENC>
-__device__ void gcm_packet(Pkt &P, const KeySlot *ks, uint32_t suite, const uint32_t *rk,
-                           int sub, uint8_t *scr, const uint8_t *lds, const LdsTe &T)
+template <int NR, bool ENC, int SUITE>
+__device__ void gcm_packet(Pkt &P, const KeySlot *ks, const uint32_t *rk, int sub, uint8_t *scr,
+                           const uint8_t *lds, const LdsTe &T)
 {
     const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4;
     const int n_g = n_a + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
@@ -265,7 +281,7 @@ __device__ void gcm_packet(Pkt &P, const KeySlot *ks, uint32_t suite, const uint
     const u32x4 tag = quad_xor_all(acc ^ ej0);
     if (ENC) {
         if (sub == 0) st16(pout + P.clen, tag);
-        if (P.hp) protect_finish_hp(P, ks, suite, sub, scr, tag, T);
+        if (P.hp) protect_finish_hp<SUITE>(P, ks, sub, scr, tag, T);
     } else {
         const u32x4 got = ld16(pin + P.clen);
         const u32x4 diff = got ^ tag;
@@ -276,8 +292,7 @@ __device__ void gcm_packet(Pkt &P, const KeySlot *ks, uint32_t suite, const uint
 // ---------------------------------------------------- ChaCha20-Poly1305 --
 
 template <bool ENC>
-__device__ void chacha_packet(Pkt &P, const KeySlot *ks, uint32_t suite, int sub, uint8_t *scr,
-                              const LdsTe &T)
+__device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
 {
     const uint32_t *key = ks->rk;
     const uint32_t n0 = P.nonce.x, n1 = P.nonce.y, n2 = P.nonce.z;
@@ -357,7 +372,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, uint32_t suite, int sub
     const u32x4 tag = p130_finish(sum, s0, s1, s2, s3);
     if (ENC) {
         if (sub == 0) st16(pout + P.clen, tag);
-        if (P.hp) protect_finish_hp(P, ks, suite, sub, scr, tag, T);
+        if (P.hp) protect_finish_hp<QPP_CHACHA20_POLY1305>(P, ks, sub, scr, tag, ConstTe{});
     } else {
         const u32x4 got = ld16(pin + P.clen);
         const u32x4 diff = got ^ tag;
@@ -365,29 +380,54 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, uint32_t suite, int sub
     }
 }
 
+template <bool ENC>
+__device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int sub, const Pkt &P)
+{
+    if (sub != 0) return;
+    const uint32_t out_len =
+        P.status == QPP_S_OK ? (uint32_t)(P.hlen + P.clen + (ENC ? QPP_TAG_LEN : 0)) : 0u;
+    res[p] = qpp_result{P.pn, (uint16_t)P.status, (uint16_t)P.hlen, out_len};
+}
+
 // ---------------------------------------------------------------- kernels --
 
-template <bool ENC>
+// One kernel per cipher suite: a launch handles the packets whose key slot
+// holds SUITE and leaves the others to the launch of their suite (the host
+// launches one kernel per suite present in the table).  Register allocation
+// is then sized for one cipher, not the union of three.
+template <int SUITE>
+struct SuiteSmem;
+template <>
+struct __attribute__((aligned(16))) SuiteSmem<QPP_AES_128_GCM> : Smem {};
+template <>
+struct __attribute__((aligned(16))) SuiteSmem<QPP_AES_256_GCM> : Smem {};
+template <>
+struct __attribute__((aligned(16))) SuiteSmem<QPP_CHACHA20_POLY1305> {
+    uint8_t scratch[kPktPerWG][kScratch];
+    uint32_t cur_slot;
+};
+
+template <int SUITE, bool ENC>
 __global__ __launch_bounds__(kWG) void k_packets(const KeySlot *__restrict__ slots,
                                                  const uint8_t *__restrict__ gtab, uint32_t cap,
                                                  const qpp_desc *__restrict__ desc, uint32_t n,
                                                  const uint8_t *gin, uint8_t *gout,
                                                  qpp_result *__restrict__ res)
 {
-    __shared__ Smem sm;
+    constexpr bool kGcm = SUITE != QPP_CHACHA20_POLY1305;
+    constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
+    __shared__ SuiteSmem<SUITE> sm;
     const int tid = threadIdx.x, sub = tid & 3, lp = tid >> 2;
-    load_te(sm);
+    if constexpr (kGcm) load_te<kWG>(sm.te);
     const uint32_t p = blockIdx.x * kPktPerWG + lp;
     const bool valid = p < n;
     qpp_desc d = {};
     if (valid) d = desc[p];
     uint32_t my_slot = valid ? d.slot : kNoSlot;
-    bool done = !valid;
-    if (valid && my_slot >= cap) {
-        if (sub == 0) res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
-        done = true;
-    }
-    const LdsTe T{sm.te, (uint32_t)(tid & 31) * 4};
+    const uint32_t my_suite = (valid && my_slot < cap) ? slots[my_slot].suite : 0xffu;
+    if (valid && my_suite > QPP_CHACHA20_POLY1305 && sub == 0)
+        res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
+    bool done = my_suite != SUITE;
     uint8_t *scr = sm.scratch[lp];
 
     for (;;) {
@@ -398,39 +438,29 @@ __global__ __launch_bounds__(kWG) void k_packets(const KeySlot *__restrict__ slo
         const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur_slot);
         if (cur == kNoSlot) break;
         const KeySlot *ks = slots + cur;
-        const uint32_t suite = __builtin_amdgcn_readfirstlane(ks->suite);
-        const bool gcm = suite == QPP_AES_128_GCM || suite == QPP_AES_256_GCM;
-        if (gcm) {
+        if constexpr (kGcm) {
             const u32x4 *src = (const u32x4 *)(gtab + (size_t)cur * kGhashTabBytes);
             for (int i = tid; i < kGhashTabBytes / 16; i += kWG) ((u32x4 *)sm.gt)[i] = src[i];
         }
         __syncthreads();
         if (!done && my_slot == cur) {
             done = true;
-            if (suite > QPP_CHACHA20_POLY1305) {
-                if (sub == 0) res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
-            } else {
-                Pkt P = pkt_begin<ENC>(d, gin, gout, ks, suite, T);
+            if constexpr (kGcm) {
+                const LdsTe T{sm.te, (uint32_t)(tid & 31) * 4};
+                Pkt P = pkt_begin<ENC, SUITE>(d, gin, gout, ks, T);
                 if (P.status == QPP_S_OK) {
-                    if (suite == QPP_AES_128_GCM) {
-                        uint32_t rk[44];
+                    uint32_t rk[4 * (kNR + 1)];
 #pragma unroll
-                        for (int i = 0; i < 44; ++i) rk[i] = __builtin_amdgcn_readfirstlane(ks->rk[i]);
-                        gcm_packet<10, ENC>(P, ks, suite, rk, sub, scr, sm.gt, T);
-                    } else if (suite == QPP_AES_256_GCM) {
-                        uint32_t rk[60];
-#pragma unroll
-                        for (int i = 0; i < 60; ++i) rk[i] = __builtin_amdgcn_readfirstlane(ks->rk[i]);
-                        gcm_packet<14, ENC>(P, ks, suite, rk, sub, scr, sm.gt, T);
-                    } else {
-                        chacha_packet<ENC>(P, ks, suite, sub, scr, T);
-                    }
+                    for (int i = 0; i < 4 * (kNR + 1); ++i)
+                        rk[i] = __builtin_amdgcn_readfirstlane(ks->rk[i]);
+                    gcm_packet<kNR, ENC, SUITE>(P, ks, rk, sub, scr, sm.gt, T);
                 }
-                if (sub == 0) {
-                    const uint32_t out_len =
-                        P.status == QPP_S_OK ? (uint32_t)(P.hlen + P.clen + (ENC ? QPP_TAG_LEN : 0)) : 0u;
-                    res[p] = qpp_result{P.pn, (uint16_t)P.status, (uint16_t)P.hlen, out_len};
-                }
+                write_result<ENC>(res, p, sub, P);
+            } else {
+                const ConstTe T;
+                Pkt P = pkt_begin<ENC, SUITE>(d, gin, gout, ks, T);
+                if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, sub, scr);
+                write_result<ENC>(res, p, sub, P);
             }
         }
         __syncthreads();
@@ -438,21 +468,24 @@ __global__ __launch_bounds__(kWG) void k_packets(const KeySlot *__restrict__ slo
 }
 
 // Header-protection masks only (HeaderProtection_mask, _crypto.c:278-287).
-__global__ __launch_bounds__(kWG) void k_hp_mask(const KeySlot *__restrict__ slots, uint32_t cap,
-                                                 const uint32_t *__restrict__ sidx,
-                                                 const uint8_t *__restrict__ samples, uint32_t n,
-                                                 uint8_t *__restrict__ masks)
+constexpr int kMaskWG = 256;
+
+__global__ __launch_bounds__(kMaskWG) void k_hp_mask(const KeySlot *__restrict__ slots,
+                                                     uint32_t cap,
+                                                     const uint32_t *__restrict__ sidx,
+                                                     const uint8_t *__restrict__ samples,
+                                                     uint32_t n, uint8_t *__restrict__ masks)
 {
-    __shared__ Smem sm;
-    load_te(sm);
+    __shared__ __attribute__((aligned(16))) uint8_t te[kTeBytes];
+    load_te<kMaskWG>(te);
     __syncthreads();
-    const LdsTe T{sm.te, (uint32_t)(threadIdx.x & 31) * 4};
-    const uint32_t i = blockIdx.x * kWG + threadIdx.x;
+    const LdsTe T{te, (uint32_t)(threadIdx.x & 31) * 4};
+    const uint32_t i = blockIdx.x * kMaskWG + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = sidx[i];
     u32x4 m = {0, 0, 0, 0};
     if (s < cap && slots[s].suite <= QPP_CHACHA20_POLY1305)
-        m = hp_mask_of(slots + s, slots[s].suite, ld16(samples + 16 * (size_t)i), T);
+        m = hp_mask_any(slots + s, slots[s].suite, ld16(samples + 16 * (size_t)i), T);
     st16(masks + 16 * (size_t)i, m);
 }
 
@@ -563,6 +596,7 @@ struct qpp_keytab {
     uint8_t *d_gtab;
     qpp_key_material *d_km;
     uint32_t km_cap;
+    uint32_t suite_mask;  // bit s set once a slot of suite s was installed
 };
 
 struct qpp_session {
@@ -651,6 +685,7 @@ int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void 
     if (n == 0) return QPP_OK;
     for (uint32_t i = 0; i < n; ++i)
         if (km[i].slot >= kt->cap || km[i].suite > QPP_CHACHA20_POLY1305) return QPP_E_ARG;
+    for (uint32_t i = 0; i < n; ++i) kt->suite_mask |= 1u << km[i].suite;
     hipStream_t s = (hipStream_t)stream;
     if (n > kt->km_cap) {
         if (kt->d_km) HIPCHK(hipFree(kt->d_km));
@@ -692,14 +727,25 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
 {
     if (!kt || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
-    const dim3 grid((n + kPktPerWG - 1) / kPktPerWG);
-    if (enc)
-        hipLaunchKernelGGL(k_packets<true>, grid, dim3(kWG), 0, (hipStream_t)stream, kt->d_slots,
-                           kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);
-    else
-        hipLaunchKernelGGL(k_packets<false>, grid, dim3(kWG), 0, (hipStream_t)stream, kt->d_slots,
-                           kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);
-    HIPCHK(hipGetLastError());
+    const dim3 grid((n + kPktPerWG - 1) / kPktPerWG), block(kWG);
+    hipStream_t s = (hipStream_t)stream;
+    // one launch per suite installed in the table (an empty table still
+    // gets one launch so every packet reports QPP_S_NO_KEY)
+    const uint32_t mask = kt->suite_mask ? kt->suite_mask : 1u;
+#define QPP_LAUNCH(SUITE)                                                                      \
+    if (mask & (1u << SUITE)) {                                                                \
+        if (enc)                                                                               \
+            hipLaunchKernelGGL((k_packets<SUITE, true>), grid, block, 0, s, kt->d_slots,       \
+                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);            \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_packets<SUITE, false>), grid, block, 0, s, kt->d_slots,      \
+                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);            \
+        HIPCHK(hipGetLastError());                                                             \
+    }
+    QPP_LAUNCH(QPP_AES_128_GCM)
+    QPP_LAUNCH(QPP_AES_256_GCM)
+    QPP_LAUNCH(QPP_CHACHA20_POLY1305)
+#undef QPP_LAUNCH
     return QPP_OK;
 }
 
@@ -720,7 +766,8 @@ int qpp_hp_mask(const qpp_keytab *kt, const uint32_t *d_slots, const uint8_t *d_
 {
     if (!kt || (n && (!d_slots || !d_samples || !d_masks))) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
-    hipLaunchKernelGGL(k_hp_mask, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_hp_mask, dim3((n + kMaskWG - 1) / kMaskWG), dim3(kMaskWG), 0,
+                       (hipStream_t)stream,
                        kt->d_slots, kt->cap, d_slots, d_samples, n, d_masks);
     HIPCHK(hipGetLastError());
     return QPP_OK;
