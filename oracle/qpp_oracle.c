@@ -545,6 +545,7 @@ void qo_unprotect_batch(const qpp_key_material *keys, uint32_t n_keys, const qpp
             r->hdr_len = d->hdr_len;
             if (m == -1) m = QO_E_LENGTH;
             else if (m == -2) m = QO_E_DECRYPT;
+            else m += d->hdr_len; /* out_len counts the copied AAD, as for protect */
         } else {
             /* key-phase check needs the unmasked first byte: remove HP first */
             uint8_t hdr[QPP_MAX_HDR + 4];

@@ -264,8 +264,15 @@ def test_aead_only_batch(oracle, L, engine_cls):
     ud["len"] = res["out_len"]
     u, r = eng.unprotect_host(ud, out.tobytes(), size)
     uo, ro = oracle.unprotect_batch(recs, ud, out, size)
-    assert (r["status"] == 0).all() and (r == ro).all()
-    assert np.array_equal(u, uo)
+    # data (ct||tag) longer than 1500 B is "Invalid payload length" (_crypto.c:126-129)
+    too_long = np.array([len(x) + 16 > 1500 for x in datas])
+    assert (r == ro).all()
+    assert ((r["status"] == L.S_LENGTH) == too_long).all()
+    assert ((r["status"] == L.S_OK) == ~too_long).all()
+    # output bytes are defined for authenticated packets only
+    for i in np.nonzero(~too_long)[0]:
+        o, ln = int(ud[i]["out_off"]), int(r[i]["out_len"])
+        assert np.array_equal(u[o : o + ln], uo[o : o + ln]), i
 
 
 def test_full_size_round_trip_64k(L, engine_cls):
