@@ -137,6 +137,16 @@ __device__ __forceinline__ uint32_t byte_of(u32x4 v, int i)
     return (w >> (8 * (i & 3))) & 0xff;
 }
 
+// Lane id recomputed where it is used (2 VALU): volatile, so the compiler
+// cannot hoist it and keep lane-derived addresses live (or spilled) across a
+// register-tight loop.
+__device__ __forceinline__ uint32_t lane_fresh()
+{
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // DPP within a quad of lanes (the 4 lanes that share one packet).
 template <int CTRL>
 __device__ __forceinline__ uint32_t quad_perm(uint32_t v)
@@ -229,12 +239,13 @@ struct ConstTe {
 // One AES encryption, state and round keys as little-endian column words.
 // Round: column c takes row r from column c+r (ShiftRows) through Te_r
 // (MixColumns coefficients); the final round substitutes only.
-template <int NR, class TE>
-__device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, const TE &T)
+// Rounds R0..NR on a state that already holds round R0-1's output.
+template <int NR, int R0, class TE>
+__device__ __forceinline__ u32x4 aes_rounds(u32x4 st, const uint32_t *rk, const TE &T)
 {
-    uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
+    uint32_t s0 = st.x, s1 = st.y, s2 = st.z, s3 = st.w;
 #pragma unroll
-    for (int r = 1; r < NR; ++r) {
+    for (int r = R0; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
         uint32_t t0 = xor3(xor3(T.t0(s0), T.t1(s1), T.t2(s2)), T.t3(s3), k[0]);
         uint32_t t1 = xor3(xor3(T.t0(s1), T.t1(s2), T.t2(s3)), T.t3(s0), k[1]);
@@ -247,6 +258,48 @@ __device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, const
                  (T.f0(s1) | T.f1(s2) | T.f2(s3) | T.f3(s0)) ^ k[1],
                  (T.f0(s2) | T.f1(s3) | T.f2(s0) | T.f3(s1)) ^ k[2],
                  (T.f0(s3) | T.f1(s0) | T.f2(s1) | T.f3(s2)) ^ k[3]};
+}
+
+template <int NR, class TE>
+__device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, const TE &T)
+{
+    return aes_rounds<NR, 1>(u32x4{in.x ^ rk[0], in.y ^ rk[1], in.z ^ rk[2], in.w ^ rk[3]}, rk, T);
+}
+
+// Counter-mode caching.  Within a packet the GCM counter block is
+// nonce || BE32(cb) with cb < 256 (at most 95 blocks + J0), so only byte 15
+// changes: in round 1 it reaches one output word through one lookup, in
+// round 2 that word reaches each output word through one lookup.  The other
+// 12 + 12 lookups are per-packet constants (c0, d0..d3): a block costs
+// 1 + 4 + 16 (NR - 2) lookups instead of 16 NR.
+struct CtrCache {
+    uint32_t c0, d0, d1, d2, d3;
+};
+
+template <class TE>
+__device__ __forceinline__ CtrCache ctr_cache(u32x4 nonce, const uint32_t *rk, const TE &T)
+{
+    const uint32_t s0 = nonce.x ^ rk[0], s1 = nonce.y ^ rk[1], s2 = nonce.z ^ rk[2], s3 = rk[3];
+    // round 1: word 0 lacks its T3(s3) term (byte 15); words 1..3 are complete
+    const uint32_t c0 = xor3(T.t0(s0), T.t1(s1), T.t2(s2)) ^ rk[4];
+    const uint32_t u1 = xor3(xor3(T.t0(s1), T.t1(s2), T.t2(s3)), T.t3(s0), rk[5]);
+    const uint32_t u2 = xor3(xor3(T.t0(s2), T.t1(s3), T.t2(s0)), T.t3(s1), rk[6]);
+    const uint32_t u3 = xor3(xor3(T.t0(s3), T.t1(s0), T.t2(s1)), T.t3(s2), rk[7]);
+    // round 2: every word lacks the one term that reads round-1 word 0
+    return CtrCache{c0, xor3(T.t1(u1), T.t2(u2), T.t3(u3)) ^ rk[8],
+                    xor3(T.t0(u1), T.t1(u2), T.t2(u3)) ^ rk[9],
+                    xor3(T.t0(u2), T.t1(u3), T.t3(u1)) ^ rk[10],
+                    xor3(T.t0(u3), T.t2(u1), T.t3(u2)) ^ rk[11]};
+}
+
+// E_K(nonce || BE32(cb)), 1 <= cb < 256, from the packet's cache
+template <int NR, class TE>
+__device__ __forceinline__ u32x4 aes_ctr(const CtrCache &c, uint32_t cb, const uint32_t *rk,
+                                         const TE &T)
+{
+    const uint32_t u0 = c.c0 ^ T.t3(rk[3] ^ (cb << 24));
+    const u32x4 v = {c.d0 ^ T.t0(u0), c.d1 ^ T.t3(u0), c.d2 ^ T.t2(u0), c.d3 ^ T.t1(u0)};
+    return aes_rounds<NR, 3>(v, rk, T);
 }
 
 // --------------------------------------------------------------- GHASH ----

@@ -27,18 +27,34 @@ namespace qpp {
 
 __constant__ AesTables c_aes = kAesTables;
 
-// One 1024-thread workgroup per CU: 16 waves (4 per SIMD, so <= 128 VGPRs)
-// share one 64 KiB AES image and one 32 KiB GHASH table set.
-constexpr int kWG = 1024;
-constexpr int kPktPerWG = kWG / 4;
-constexpr int kScratch = 48;  // (ct||tag)[0..48) per packet, for the HP sample
+// GCM: one workgroup per CU shares one 64 KiB AES image and one 32 KiB GHASH
+// table set; the workgroup size sets the waves per SIMD (and so the VGPR
+// budget): 512 -> 2 (256 VGPRs), 768 -> 3 (168), 1024 -> 4 (128).
+// ChaCha20-Poly1305 needs no tables.  4 lanes per packet in every case.
+constexpr int kSetupWG = 256;
+// Per-packet LDS scratch: [0, 32) ct[0..32) (+ tag) for the protect HP
+// sample; [32, 48) tiny-input staging, then the partial tail block; [48, 64)
+// E_K(J0); [64, 96) the parked packet view (GCM step loop).
+constexpr int kScratch = 96;
+constexpr int kScrTail = 32, kScrEj0 = 48, kScrPark = 64;
+constexpr int kStageBytes = 64 * 16;  // one 16-byte block per lane of a wave
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
-struct __attribute__((aligned(16))) Smem {
+template <int WG>
+struct __attribute__((aligned(16))) GcmSmem {
     uint8_t te[kTeBytes];             // Te0|Te1 x 32 bank copies   64 KiB
     uint8_t gt[kGhashTabBytes];       // GHASH H^1..H^4 tables      32 KiB
-    uint8_t scratch[kPktPerWG][kScratch];
-    uint32_t cur_slot;
+    uint8_t scratch[WG / 4][kScratch];
+    unsigned long long base_in, base_out;
+    uint8_t stage[WG / 64][2][kStageBytes];  // per-wave LDS-DMA input staging
+    uint32_t cur_slot[2];
+};
+
+template <int WG>
+struct __attribute__((aligned(16))) ChachaSmem {
+    uint8_t scratch[WG / 4][kScratch];
+    unsigned long long base_in, base_out;
+    uint32_t cur_slot[2];
 };
 
 // Fill the LDS AES image: row x = [Te0[x] x 32 | Te1[x] x 32], 16-byte stores.
@@ -141,9 +157,39 @@ struct Pkt {
 
 // Header analysis shared by both suites.  Unprotect removes header
 // protection here (it decides the header length and the packet number).
+// Header bytes that header protection needs, requested with the descriptor
+// (before the key slot is known): byte 0 and, for unprotect, the packet-number
+// bytes and the sample.  Reads only what pkt_begin's length checks allow.
+struct HdrPre {
+    u32x4 h0;        // input bytes [0, 16) when the readable region holds them
+    u32x4 pnw, smp;  // unprotect: packet-number bytes, sample
+    uint32_t b0;
+};
+
+template <bool ENC>
+__device__ __forceinline__ HdrPre prefetch_hdr(const qpp_desc &d, const uint8_t *gin, bool valid)
+{
+    HdrPre r = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, 0};
+    if (!valid) return r;
+    const uint8_t *src = gin + d.in_off;
+    const bool hp = !(d.flags & QPP_F_NO_HP) && d.hdr_len >= 1;
+    const uint64_t region = ENC ? (uint64_t)d.hdr_len + d.len : (uint64_t)d.len;
+    if (region >= 16) {
+        r.h0 = ld16(src);
+        r.b0 = r.h0.x & 0xff;
+    } else if (hp) {
+        r.b0 = src[0];
+    }
+    if (!ENC && hp && (int)d.hdr_len + 20 <= (int)d.len && d.hdr_len <= QPP_MAX_HDR - 4) {
+        r.pnw = ld16(src + d.hdr_len);
+        r.smp = ld16(src + d.hdr_len + 4);
+    }
+    return r;
+}
+
 template <bool ENC, int SUITE, class TE>
-__device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const uint8_t *gin, uint8_t *gout,
-                                         const KeySlot *ks, const TE &T)
+__device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const HdrPre &pre, const uint8_t *gin,
+                                         uint8_t *gout, const KeySlot *ks, const TE &T)
 {
     Pkt P;
     P.src = gin + d.in_off;
@@ -166,7 +212,7 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const uint8_t *gin, 
             if (P.hlen < 1) {
                 P.status = QPP_S_LENGTH;
             } else {
-                uint32_t b0 = P.src[0];
+                const uint32_t b0 = pre.b0;
                 P.pn_len = (int)(b0 & 3) + 1;
                 P.pn_off = P.hlen - P.pn_len;
                 P.fbm = first_byte_mask(b0);
@@ -180,16 +226,14 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const uint8_t *gin, 
         if (P.pn_off < 1 || P.pn_off + 20 > len || P.pn_off > QPP_MAX_HDR - 4) {
             P.status = QPP_S_LENGTH;
         } else {
-            const u32x4 sample = ld16(P.src + P.pn_off + 4);
-            P.mask = hp_mask_of<SUITE>(ks, sample, T);
-            uint32_t b0 = P.src[0];
+            P.mask = hp_mask_of<SUITE>(ks, pre.smp, T);
+            uint32_t b0 = pre.b0;
             P.fbm = first_byte_mask(b0);
             b0 ^= byte_of(P.mask, 0) & P.fbm;
             P.pn_len = (int)(b0 & 3) + 1;
-            const u32x4 pnw = ld16(P.src + P.pn_off);
             uint32_t trunc = 0;
             for (int i = 0; i < P.pn_len; ++i)
-                trunc = (trunc << 8) | (byte_of(pnw, i) ^ byte_of(P.mask, 1 + i));
+                trunc = (trunc << 8) | (byte_of(pre.pnw, i) ^ byte_of(P.mask, 1 + i));
             P.pn = decode_pn(trunc, P.pn_len, d.pn, d.flags & QPP_F_RFC_PN);
             P.hlen = P.pn_off + P.pn_len;
             const int body = len - P.hlen;
@@ -218,7 +262,7 @@ __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int
 {
     // sample = (ct||tag)[4-pn_len : 20-pn_len]; the tag only matters when clen < 20
     if (P.clen < 32 && sub == 0) {
-        for (int j = 0; j < 16 && P.clen + j < kScratch; ++j)
+        for (int j = 0; j < 16 && P.clen + j < 32; ++j)
             scr[P.clen + j] = (uint8_t)byte_of(tag, j);
     }
     __builtin_amdgcn_wave_barrier();
@@ -233,59 +277,255 @@ __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int
     }
 }
 
+// Header out: the plain header (unprotect), or the input header with the HP
+// mask applied (protect).  Outside the step loop; byte tails allowed here.
+__device__ __forceinline__ void write_header(const Pkt &P, int sub, bool masked)
+{
+    const int n_a = (P.hlen + 15) >> 4;
+    for (int q = sub; q < n_a; q += 4) {
+        const int nb = min(16, P.hlen - 16 * q);
+        u32x4 h = ld_part(P.src + 16 * q, nb);
+        if (masked) h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
+        st_part(P.dst + 16 * q, h, nb);
+    }
+}
+
+// 128-bit little-endian shift right by s bytes (0..15)
+__device__ __forceinline__ u32x4 shr_bytes(u32x4 v, int s)
+{
+    uint64_t lo = (uint64_t)v.y << 32 | v.x, hi = (uint64_t)v.w << 32 | v.z;
+    if (s >= 8) {
+        lo = hi >> (8 * (s - 8));
+        hi = 0;
+    } else if (s > 0) {
+        lo = (lo >> (8 * s)) | (hi << (64 - 8 * s));
+        hi >>= 8 * s;
+    }
+    return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// 128-bit little-endian shift left by s bytes (0..15)
+__device__ __forceinline__ u32x4 shl_bytes(u32x4 v, int s)
+{
+    uint64_t lo = (uint64_t)v.y << 32 | v.x, hi = (uint64_t)v.w << 32 | v.z;
+    if (s >= 8) {
+        hi = lo << (8 * (s - 8));
+        lo = 0;
+    } else if (s > 0) {
+        hi = (hi << (8 * s)) | (lo >> (64 - 8 * s));
+        lo <<= 8 * s;
+    }
+    return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// Buffer descriptors over the whole input / output buffers.  Offsets at or
+// above kOob are out of range: loads return zeros, stores are dropped.  This
+// lets every step issue exactly one load and one store per lane with no
+// branch around them, so the compiler can count vmcnt instead of draining.
+constexpr uint32_t kBufBytes = 0xffffff00u;
+constexpr uint32_t kOob = 0xfffffff0u;
+
+struct Bufs {
+    __amdgpu_buffer_rsrc_t in, out;
+};
+
 // --------------------------------------------------------------- AES-GCM --
 
-template <int NR, bool ENC, int SUITE>
-__device__ void gcm_packet(Pkt &P, const KeySlot *ks, const uint32_t *rk, int sub, uint8_t *scr,
-                           const uint8_t *lds, const LdsTe &T)
-{
-    const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4;
-    const int n_g = n_a + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
-    const u32x4 j0 = u32x4{P.nonce.x, P.nonce.y, P.nonce.z, 0x01000000u};
-    const uint64_t abits = (uint64_t)P.hlen * 8, cbits = (uint64_t)P.clen * 8;
-    const uint8_t *pin = P.src + P.hlen;
-    uint8_t *pout = P.dst + P.hlen;
-    const bool unmask = !ENC && P.hp;
-    constexpr uint32_t kTabH4 = 3 * 8192;
-    u32x4 acc = {0, 0, 0, 0}, ej0 = {0, 0, 0, 0};
+// Phase timestamps per wave (tools/probe.hip builds with -DQPP_PROBE):
+// 100 MHz s_memrealtime, written by the wave's first active lane.
+#ifdef QPP_PROBE
+constexpr int kProbeSlots = 16;
+__device__ unsigned long long g_probe[8192 * kProbeSlots];
+#define QPP_PROBE_AT(i)                                                                      \
+    do {                                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                      \
+        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                              \
+            g_probe[(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * kProbeSlots + (i)] = t_; \
+    } while (0)
+#else
+#define QPP_PROBE_AT(i) ((void)0)
+#endif
 
-    for (int k = 0; k < S; ++k) {
-        const int g = 4 * k + sub - pad, i = g - n_a;
-        u32x4 ctr = j0;
-        if (i >= 0 && i < n_c) ctr.w = bswap((uint32_t)(i + 2));
-        const u32x4 ksb = aes_encrypt<NR>(ctr, rk, T);
-        u32x4 x = {0, 0, 0, 0};
-        if (g >= 0 && g < n_a) {
-            // associated data = the (plain) header
-            const int nb = min(16, P.hlen - 16 * g);
-            x = ld_part(P.src + 16 * g, nb);
-            if (unmask) x ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
-            if (!ENC || !P.hp) st_part(P.dst + 16 * g, x, nb);
-        } else if (i >= 0 && i < n_c) {
-            const int nb = min(16, P.clen - 16 * i);
-            const u32x4 din = ld_part(pin + 16 * i, nb);
-            const u32x4 dout = din ^ ksb;
-            st_part(pout + 16 * i, dout, nb);
-            x = keep_bytes(ENC ? dout : din, nb);
-            if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x;
-        } else if (i == n_c) {
-            // lengths block; this lane's AES slot produced E_K(J0) for the tag
-            x = u32x4{bswap((uint32_t)(abits >> 32)), bswap((uint32_t)abits),
-                      bswap((uint32_t)(cbits >> 32)), bswap((uint32_t)cbits)};
-            ej0 = ksb;
+// Per-packet state that the GCM step loop does not touch waits in LDS
+// (scratch [64, 96)) while the loop runs, so the loop keeps its 128 VGPRs.
+__device__ __forceinline__ void park(const Pkt &P, uint8_t *scr)
+{
+    *(u32x4 *)(scr + kScrPark) = P.mask;
+    *(u32x4 *)(scr + kScrPark + 16) =
+        u32x4{(uint32_t)P.pn, (uint32_t)(P.pn >> 32),
+              P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28, 0};
+}
+__device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, uint8_t *dst, int hlen,
+                                      int clen)
+{
+    Pkt P;
+    const u32x4 w = *(const u32x4 *)(scr + kScrPark + 16);
+    P.src = src;
+    P.dst = dst;
+    P.hlen = hlen;
+    P.clen = clen;
+    P.mask = *(const u32x4 *)(scr + kScrPark);
+    P.pn = (uint64_t)w.y << 32 | w.x;
+    P.fbm = w.z & 0xff;
+    P.pn_off = (int)((w.z >> 8) & 0xffff);
+    P.pn_len = (int)((w.z >> 24) & 0xf);
+    P.hp = (w.z >> 28) & 1;
+    P.status = QPP_S_OK;
+    P.nonce = u32x4{0, 0, 0, 0};
+    return P;
+}
+
+// AES-GCM of one packet by its quad (SP 800-38D; _crypto.c:157-204 / :115-155).
+//   * The associated data (header) is first folded to one block
+//     Z = sum_g A_g H^(n_a-1-g) by every lane of the quad; GHASH is linear, so
+//     Z then stands for the whole header as the first block of the sequence
+//     [Z | CT | lengths] that the step loop walks (front-padded to 4S).
+//   * Step k: lane `sub` owns block 4k+sub: one AES-CTR block (rounds 1-2 from
+//     the packet's counter cache), one LDS-DMA load of next step's input
+//     block (the received tag on the last step) into the wave's staging
+//     buffer, one buffer store (dropped out of range for partial blocks), one
+//     H^4 multiply.
+//   * Partial tail block -> LDS, E_K(J0) -> LDS; both go out after the loop.
+// The input region holds >= 16 bytes except for tiny protects, which are
+// staged in LDS.  Returns the tag; got_tag = the received tag (unprotect).
+// Inside the step loop every lane-derived address (LDS table lane offset,
+// staging slot, packet scratch) is recomputed from lane_fresh(): 128 VGPRs
+// leave no room to keep them live.  scr_wave = the wave's 16 packet
+// scratches, stage = the wave's 2 staging buffers, te = the AES image.
+template <int NR, bool ENC>
+__device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int clen,
+                                            const uint32_t *rk, int sub, uint8_t *scr,
+                                            uint8_t *scr_wave, const uint8_t *lds,
+                                            const uint8_t *te, const Bufs &B,
+                                            const uint8_t *src, uint32_t ioff, uint32_t ooff,
+                                            const u32x4 hmask, const uint32_t hbits, const u32x4 h0,
+                                            uint8_t *stage, u32x4 &got_tag)
+{
+    const LdsTe T{te, (uint32_t)(threadIdx.x & 31) * 4};
+    const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
+    const int n_g = za + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
+    const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
+    const bool tiny = rlen < 16;
+    constexpr uint32_t kTabH4 = 3 * 8192;
+
+    if (tiny) *(u32x4 *)(scr + kScrTail) = ld_part(src, rlen);
+
+    // fold the associated data (unmasked for unprotect) into Z
+    u32x4 z = {0, 0, 0, 0};
+    for (int g = 0; g < n_a; ++g) {
+        u32x4 a;
+        if (tiny) {
+            a = *(const u32x4 *)(scr + kScrTail);
+        } else if (g == 0) {
+            a = h0;  // requested with the descriptor
+        } else {
+            // 16 bytes at region offset 16 g: end-aligned load + shift
+            const int ld = min(16 * g, rlen - 16);
+            a = shr_bytes(__builtin_amdgcn_raw_buffer_load_b128(B.in, (int)(ioff + ld), 0, 0),
+                          16 * g - ld);
         }
-        acc ^= x;
-        if (k < S - 1) acc = ghash_mul(acc, lds, kTabH4);
-        else acc = ghash_mul(acc, lds, (uint32_t)(3 - sub) * 8192u);
+        a = keep_bytes(a, min(16, hlen - 16 * g));
+        if (!ENC && (hbits >> 28))
+            a ^= hp_pattern(16 * g, hmask, hbits & 0xff, (hbits >> 8) & 0xffff, (hbits >> 24) & 0xf);
+        if (g > 0) z = ghash_mul(z, lds, 0);
+        z ^= a;
     }
-    const u32x4 tag = quad_xor_all(acc ^ ej0);
-    if (ENC) {
-        if (sub == 0) st16(pout + P.clen, tag);
-        if (P.hp) protect_finish_hp<SUITE>(P, ks, sub, scr, tag, T);
+    u32x4 acc = (za && sub == pad) ? z : u32x4{0, 0, 0, 0};
+    const int q = pad + za;  // sequence position of CT block 0
+    // E_K(J0) slot starts at zero: lanes other than the lengths lane add 0
+    *(u32x4 *)(scr + kScrEj0) = u32x4{0, 0, 0, 0};
+    const CtrCache cc = ctr_cache(nonce, rk, T);
+    const uint32_t lens_h = bswap((uint32_t)hlen * 8u);
+    const uint32_t cin = ioff + (uint32_t)hlen, cout = ooff + (uint32_t)hlen;
+
+    // one block of the sequence: CT block i (input `raw` loaded from CT offset
+    // min(16 i, clen - 16) for protect, i.e. end-aligned for a partial tail),
+    // the lengths block (i == n_c), or padding
+    auto step = [&](int i, bool last, u32x4 raw) {
+        const bool is_ct = i >= 0 && 16 * i < clen;
+        const LdsTe Tl{te, (lane_fresh() & 31) * 4};
+        const u32x4 ksb = aes_ctr<NR>(cc, is_ct ? (uint32_t)(i + 2) : 1u, rk, Tl);
+        u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
+        uint32_t soff = kOob;
+        if (is_ct) {
+            const int nb = min(16, clen - 16 * i);
+            const u32x4 cur = (ENC && nb < 16) ? shr_bytes(raw, 16 - nb) : raw;
+            out = cur ^ ksb;
+            x = keep_bytes(ENC ? out : cur, nb);
+            uint8_t *ps = scr_wave + (lane_fresh() >> 2) * kScratch;
+            if (nb == 16) soff = cout + 16u * (uint32_t)i;
+            else *(u32x4 *)(ps + kScrTail) = out;
+            if (ENC && i < 2) *(u32x4 *)(ps + 16 * i) = x;
+        } else if (i >= 0 && 16 * i < clen + 16) {
+            // lengths block; this lane's AES slot produced E_K(J0) for the tag
+            x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
+            *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, 0);
+        acc ^= x;
+        // AES and GHASH of a step are independent for unprotect; overlapping
+        // them would need more than the 128 VGPRs of 4 waves/SIMD
+        __builtin_amdgcn_sched_barrier(0);
+        acc = ghash_mul(acc, lds, last ? (3u - (lane_fresh() & 3)) * 8192u : kTabH4);
+    };
+    // buffer offset of CT block i's input (or out of range)
+    auto ct_load = [&](int i) -> uint32_t {
+        if (i < 0 || 16 * i >= clen) return kOob;
+        return cin + (uint32_t)(ENC ? min(16 * i, clen - 16) : 16 * i);
+    };
+
+    got_tag = u32x4{0, 0, 0, 0};
+    if (tiny) {
+        // < 16 input bytes: one step (n_a, n_c <= 1), input from LDS
+        QPP_PROBE_AT(3);
+        // the staged bytes as an end-aligned load would see them
+        const u32x4 st = *(const u32x4 *)(scr + kScrTail);
+        step(sub - q, true, shl_bytes(st, 16 - rlen));
     } else {
-        const u32x4 got = ld16(pin + P.clen);
-        const u32x4 diff = got ^ tag;
+        // LDS-DMA staging: lane l's 16 bytes land at stage[buf][16 l]
+        auto dma = [&](uint32_t off, int buf) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                B.in, (__attribute__((address_space(3))) void *)(stage + buf * kStageBytes), 16,
+                off, 0, 0, 0);
+        };
+        int i = sub - q, b = 0;
+        dma(ct_load(i), 0);
+        QPP_PROBE_AT(3);
+        for (int k = S; k > 0; --k, i += 4, b ^= 1) {
+            // the compiler does not track LDS-DMA: retire it explicitly
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const u32x4 raw = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
+            // next step's block; on the last step the received tag
+            dma((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4), b ^ 1);
+            step(i, k == 1, raw);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
+    }
+    // the lengths block is the last of the sequence: lane 3, last step
+    __builtin_amdgcn_wave_barrier();
+    if (sub == 3) acc ^= *(const u32x4 *)(scr + kScrEj0);
+    return quad_xor_all(acc);
+}
+
+// Output side of a GCM packet after the step loop: partial tail block, tag,
+// header (with header protection for protect), tag check for unprotect.
+template <bool ENC, int SUITE>
+__device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr,
+                                           const LdsTe &T, u32x4 tag, u32x4 got_tag)
+{
+    const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
+    const int n_g = za + n_c + 1, pad = 4 * ((n_g + 3) >> 2) - n_g;
+    if ((P.clen & 15) && sub == ((pad + za + n_c - 1) & 3))
+        st_part(P.dst + P.hlen + 16 * (n_c - 1), *(const u32x4 *)(scr + kScrTail), P.clen & 15);
+    if (ENC) {
+        if (sub == 0) st16(P.dst + P.hlen + P.clen, tag);
+        if (P.hp) protect_finish_hp<SUITE>(P, ks, sub, scr, tag, T);
+        else write_header(P, sub, false);
+    } else {
+        const u32x4 diff = got_tag ^ tag;
         if ((diff.x | diff.y | diff.z | diff.w) != 0) P.status = QPP_S_DECRYPT;
+        write_header(P, sub, P.hp);
     }
 }
 
@@ -324,8 +564,20 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
             g_last = g;
         }
     }
+    // the 64 input bytes of chunk c, fetched one chunk ahead of use
+    auto fetch = [&](int c, u32x4 (&v)[4]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i = 4 * c + t;
+            v[t] = i < n_c ? ld_part(pin + 16 * i, min(16, P.clen - 16 * i)) : u32x4{0, 0, 0, 0};
+        }
+    };
+    u32x4 nxt[4];
+    if (sub < chunks) fetch(sub, nxt);
     // acc already carries one factor r per folded block: h = (h + m) * r
     for (int c = sub; c < chunks; c += 4) {
+        u32x4 cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+        if (c + 4 < chunks) fetch(c + 4, nxt);
         chacha_block(key, (uint32_t)(1 + c), n0, n1, n2, blk);
         // jump from this lane's previous block to the first block of chunk c
         if (g_last >= 0 && c >= 4) acc = p130_mul(acc, r12);  // gap of 13 blocks: r^12, then r^1 per block
@@ -334,7 +586,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
             const int i = 4 * c + t;
             if (i >= n_c) break;
             const int nb = min(16, P.clen - 16 * i);
-            const u32x4 din = ld_part(pin + 16 * i, nb);
+            const u32x4 din = cur[t];
             const u32x4 ksb = u32x4{blk[4 * t], blk[4 * t + 1], blk[4 * t + 2], blk[4 * t + 3]};
             const u32x4 dout = din ^ ksb;
             st_part(pout + 16 * i, dout, nb);
@@ -395,76 +647,127 @@ __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int su
 // holds SUITE and leaves the others to the launch of their suite (the host
 // launches one kernel per suite present in the table).  Register allocation
 // is then sized for one cipher, not the union of three.
-template <int SUITE>
-struct SuiteSmem;
-template <>
-struct __attribute__((aligned(16))) SuiteSmem<QPP_AES_128_GCM> : Smem {};
-template <>
-struct __attribute__((aligned(16))) SuiteSmem<QPP_AES_256_GCM> : Smem {};
-template <>
-struct __attribute__((aligned(16))) SuiteSmem<QPP_CHACHA20_POLY1305> {
-    uint8_t scratch[kPktPerWG][kScratch];
-    uint32_t cur_slot;
-};
+template <int SUITE, int WG>
+using SuiteSmem =
+    typename std::conditional<SUITE == QPP_CHACHA20_POLY1305, ChachaSmem<WG>, GcmSmem<WG>>::type;
 
-template <int SUITE, bool ENC>
-__global__ __launch_bounds__(kWG) void k_packets(const KeySlot *__restrict__ slots,
-                                                 const uint8_t *__restrict__ gtab, uint32_t cap,
-                                                 const qpp_desc *__restrict__ desc, uint32_t n,
-                                                 const uint8_t *gin, uint8_t *gout,
-                                                 qpp_result *__restrict__ res)
+
+template <int SUITE, bool ENC, int WG>
+__global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slots,
+                                                const uint8_t *__restrict__ gtab, uint32_t cap,
+                                                const qpp_desc *__restrict__ desc, uint32_t n,
+                                                const uint8_t *gin, uint8_t *gout,
+                                                qpp_result *__restrict__ res)
 {
     constexpr bool kGcm = SUITE != QPP_CHACHA20_POLY1305;
     constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
-    __shared__ SuiteSmem<SUITE> sm;
+    constexpr int kPktPerWG = WG / 4;
+    __shared__ SuiteSmem<SUITE, WG> sm;
     const int tid = threadIdx.x, sub = tid & 3, lp = tid >> 2;
-    if constexpr (kGcm) load_te<kWG>(sm.te);
     const uint32_t p = blockIdx.x * kPktPerWG + lp;
     const bool valid = p < n;
+    uint8_t *scr = sm.scratch[lp];
+    QPP_PROBE_AT(0);
+
+    // Prologue: everything that depends only on the descriptor is requested
+    // at once (descriptor, then the header bytes that header protection needs),
+    // and the key slot is picked with one LDS min-reduction.  Each dependent
+    // global access costs microseconds at launch, when every CU issues at once.
     qpp_desc d = {};
     if (valid) d = desc[p];
-    uint32_t my_slot = valid ? d.slot : kNoSlot;
-    const uint32_t my_suite = (valid && my_slot < cap) ? slots[my_slot].suite : 0xffu;
-    if (valid && my_suite > QPP_CHACHA20_POLY1305 && sub == 0)
-        res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
-    bool done = my_suite != SUITE;
-    uint8_t *scr = sm.scratch[lp];
+    if (tid == 0) {
+        sm.cur_slot[0] = kNoSlot;
+        sm.base_in = sm.base_out = ~0ull;
+    }
+    if constexpr (kGcm) load_te<WG>(sm.te);
+    const HdrPre pre = prefetch_hdr<ENC>(d, gin, valid);
+    __syncthreads();
+    const uint32_t my_slot = valid ? d.slot : kNoSlot;
+    bool done = !valid;
+    if (valid) {
+        atomicMin(&sm.cur_slot[0], my_slot);
+        atomicMin(&sm.base_in, (unsigned long long)d.in_off);
+        atomicMin(&sm.base_out, (unsigned long long)d.out_off);
+    }
+    __syncthreads();
+    QPP_PROBE_AT(7);
+    // 32-bit buffer views based at this workgroup's lowest input / output
+    // offsets (a workgroup's packets must lie within 4 GiB of each other)
+    const uint64_t bi = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sm.base_in >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)sm.base_in);
+    const uint64_t bo = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sm.base_out >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)sm.base_out);
 
-    for (;;) {
-        if (tid == 0) sm.cur_slot = kNoSlot;
-        __syncthreads();
-        if (!done) atomicMin(&sm.cur_slot, my_slot);
-        __syncthreads();
-        const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur_slot);
+    // one iteration per distinct key slot in the workgroup, lowest first;
+    // cur_slot is double-buffered so the next minimum is reduced meanwhile
+    for (int it = 0;; ++it) {
+        const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur_slot[it & 1]);
         if (cur == kNoSlot) break;
         const KeySlot *ks = slots + cur;
+        const uint32_t suite = cur < cap ? ks->suite : 0xffu;
+        const bool mine = suite == SUITE;
+        if (tid == 0) sm.cur_slot[(it + 1) & 1] = kNoSlot;
         if constexpr (kGcm) {
-            const u32x4 *src = (const u32x4 *)(gtab + (size_t)cur * kGhashTabBytes);
-            for (int i = tid; i < kGhashTabBytes / 16; i += kWG) ((u32x4 *)sm.gt)[i] = src[i];
+            if (mine) {
+                const u32x4 *src = (const u32x4 *)(gtab + (size_t)cur * kGhashTabBytes);
+                for (int i = tid; i < kGhashTabBytes / 16; i += WG) ((u32x4 *)sm.gt)[i] = src[i];
+            }
         }
         __syncthreads();
-        if (!done && my_slot == cur) {
-            done = true;
+        QPP_PROBE_AT(1);
+        const bool in_slot = !done && my_slot == cur;
+        done = done || in_slot;
+        if (!done) atomicMin(&sm.cur_slot[(it + 1) & 1], my_slot);
+        if (in_slot && suite > QPP_CHACHA20_POLY1305 && sub == 0)
+            res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
+        if (in_slot && mine) {
             if constexpr (kGcm) {
                 const LdsTe T{sm.te, (uint32_t)(tid & 31) * 4};
-                Pkt P = pkt_begin<ENC, SUITE>(d, gin, gout, ks, T);
+                Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
                 if (P.status == QPP_S_OK) {
                     uint32_t rk[4 * (kNR + 1)];
 #pragma unroll
                     for (int i = 0; i < 4 * (kNR + 1); ++i)
                         rk[i] = __builtin_amdgcn_readfirstlane(ks->rk[i]);
-                    gcm_packet<kNR, ENC, SUITE>(P, ks, rk, sub, scr, sm.gt, T);
+                    const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
+                    const uint64_t rlen = (uint64_t)(P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN));
+                    const uint64_t wlen = (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN);
+                    if (ioff + rlen <= kBufBytes && ooff + wlen <= kBufBytes) {
+                        const Bufs B{
+                            __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
+                            __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
+                        const uint8_t *src = P.src;
+                        const int hlen = P.hlen, clen = P.clen;
+                        const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 |
+                                               (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28;
+                        park(P, scr);
+                        QPP_PROBE_AT(2);
+                        u32x4 got_tag;
+                        const u32x4 tag = gcm_packet<kNR, ENC>(
+                            P.nonce, hlen, clen, rk, sub, scr, sm.scratch[__builtin_amdgcn_readfirstlane(tid >> 6) * 16], sm.gt,
+                            sm.te, B, src, (uint32_t)ioff,
+                            (uint32_t)ooff, P.mask, hbits, pre.h0,
+                            sm.stage[__builtin_amdgcn_readfirstlane(tid >> 6)][0],
+                            got_tag);
+                        QPP_PROBE_AT(4);
+                        P = unpark(scr, gin + bi + ioff, gout + bo + ooff, hlen, clen);
+                        gcm_finish<ENC, SUITE>(P, ks, sub, scr, T, tag, got_tag);
+                    } else {
+                        P.status = QPP_S_LENGTH;  // workgroup spans more than 4 GiB
+                    }
                 }
                 write_result<ENC>(res, p, sub, P);
+                QPP_PROBE_AT(5);
             } else {
                 const ConstTe T;
-                Pkt P = pkt_begin<ENC, SUITE>(d, gin, gout, ks, T);
+                Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
                 if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, sub, scr);
                 write_result<ENC>(res, p, sub, P);
             }
         }
         __syncthreads();
     }
+    QPP_PROBE_AT(6);
 }
 
 // Header-protection masks only (HeaderProtection_mask, _crypto.c:278-287).
@@ -523,7 +826,7 @@ __device__ __forceinline__ uint32_t le32(const uint8_t *p)
 
 // One workgroup per key: round keys / ChaCha keys, H = E_K(0^128), H^2..H^4
 // and the 2048 GHASH table entries (AEAD_init + HeaderProtection_init).
-__global__ __launch_bounds__(kWG) void k_key_setup(KeySlot *__restrict__ slots,
+__global__ __launch_bounds__(kSetupWG) void k_key_setup(KeySlot *__restrict__ slots,
                                                    uint8_t *__restrict__ gtab, uint32_t cap,
                                                    const qpp_key_material *__restrict__ km,
                                                    uint32_t n)
@@ -559,11 +862,11 @@ __global__ __launch_bounds__(kWG) void k_key_setup(KeySlot *__restrict__ slots,
     }
     __syncthreads();
     KeySlot *dst = slots + m.slot;
-    for (int i = threadIdx.x; i < (int)(sizeof(KeySlot) / 4); i += kWG)
+    for (int i = threadIdx.x; i < (int)(sizeof(KeySlot) / 4); i += kSetupWG)
         ((uint32_t *)dst)[i] = ((const uint32_t *)&ks)[i];
     if (m.suite == QPP_AES_128_GCM || m.suite == QPP_AES_256_GCM) {
         u32x4 *tab = (u32x4 *)(gtab + (size_t)m.slot * kGhashTabBytes);
-        for (int e = threadIdx.x; e < kGhashPowers * 32 * 16; e += kWG) {
+        for (int e = threadIdx.x; e < kGhashPowers * 32 * 16; e += kSetupWG) {
             const int p = e >> 9, w = (e >> 4) & 31, v = e & 15;
             // element with nibble v at window w: byte w/2, low (w even) or high nibble
             uint32_t words[4] = {0, 0, 0, 0};
@@ -696,7 +999,7 @@ int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void 
     }
     HIPCHK(hipMemcpyAsync(kt->d_km, km, (size_t)n * sizeof(qpp_key_material),
                           hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_key_setup, dim3(n), dim3(kWG), 0, s, kt->d_slots, kt->d_gtab, kt->cap,
+    hipLaunchKernelGGL(k_key_setup, dim3(n), dim3(kSetupWG), 0, s, kt->d_slots, kt->d_gtab, kt->cap,
                        kt->d_km, n);
     HIPCHK(hipGetLastError());
     // key material is host memory owned by the caller: finish before returning
@@ -722,30 +1025,52 @@ int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *st
     return e == hipSuccess ? QPP_OK : QPP_E_HIP;
 }
 
+// Workgroup size per suite family (tuned on MI355X; overridable for sweeps
+// with QPP_WG_GCM / QPP_WG_CHACHA = 512 | 768 | 1024).
+static const int kGcmWG = 1024;
+static const int kChachaWG = 512;
+
+static int wg_choice(const char *env, int dflt)
+{
+    const char *v = getenv(env);
+    if (!v) return dflt;
+    const int w = atoi(v);
+    return (w == 512 || w == 768 || w == 1024) ? w : dflt;
+}
+
+
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                           const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream)
 {
     if (!kt || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
-    const dim3 grid((n + kPktPerWG - 1) / kPktPerWG), block(kWG);
     hipStream_t s = (hipStream_t)stream;
     // one launch per suite installed in the table (an empty table still
     // gets one launch so every packet reports QPP_S_NO_KEY)
     const uint32_t mask = kt->suite_mask ? kt->suite_mask : 1u;
-#define QPP_LAUNCH(SUITE)                                                                      \
-    if (mask & (1u << SUITE)) {                                                                \
+    const int wg_gcm = wg_choice("QPP_WG_GCM", kGcmWG), wg_cc = wg_choice("QPP_WG_CHACHA", kChachaWG);
+#define QPP_LAUNCH_WG(SUITE, WGV)                                                              \
+    do {                                                                                       \
+        const dim3 grid((n + WGV / 4 - 1) / (WGV / 4)), block(WGV);                            \
         if (enc)                                                                               \
-            hipLaunchKernelGGL((k_packets<SUITE, true>), grid, block, 0, s, kt->d_slots,       \
+            hipLaunchKernelGGL((k_packets<SUITE, true, WGV>), grid, block, 0, s, kt->d_slots,  \
                                kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);            \
         else                                                                                   \
-            hipLaunchKernelGGL((k_packets<SUITE, false>), grid, block, 0, s, kt->d_slots,      \
+            hipLaunchKernelGGL((k_packets<SUITE, false, WGV>), grid, block, 0, s, kt->d_slots, \
                                kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);            \
+    } while (0)
+#define QPP_LAUNCH(SUITE, WGSEL)                                                               \
+    if (mask & (1u << SUITE)) {                                                                \
+        if (WGSEL == 512) QPP_LAUNCH_WG(SUITE, 512);                                           \
+        else if (WGSEL == 768) QPP_LAUNCH_WG(SUITE, 768);                                      \
+        else QPP_LAUNCH_WG(SUITE, 1024);                                                       \
         HIPCHK(hipGetLastError());                                                             \
     }
-    QPP_LAUNCH(QPP_AES_128_GCM)
-    QPP_LAUNCH(QPP_AES_256_GCM)
-    QPP_LAUNCH(QPP_CHACHA20_POLY1305)
+    QPP_LAUNCH(QPP_AES_128_GCM, wg_gcm)
+    QPP_LAUNCH(QPP_AES_256_GCM, wg_gcm)
+    QPP_LAUNCH(QPP_CHACHA20_POLY1305, wg_cc)
 #undef QPP_LAUNCH
+#undef QPP_LAUNCH_WG
     return QPP_OK;
 }
 
