@@ -147,6 +147,27 @@ __device__ __forceinline__ uint32_t lane_fresh()
     return l;
 }
 
+// Wave-wide minimum (every lane gets it), by xor-shuffles: lane-serialized
+// LDS atomics on one word cost ~4 cycles per lane, 64 times per wave.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
+        const uint64_t w = (uint64_t)hi << 32 | lo;
+        v = w < v ? w : v;
+    }
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32 |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 // DPP within a quad of lanes (the 4 lanes that share one packet).
 template <int CTRL>
 __device__ __forceinline__ uint32_t quad_perm(uint32_t v)

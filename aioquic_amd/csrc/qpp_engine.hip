@@ -53,7 +53,6 @@ struct __attribute__((aligned(16))) GcmSmem {
 template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
     uint8_t scratch[WG / 4][kScratch];
-    unsigned long long base_in, base_out;
     uint32_t cur_slot[2];
 };
 
@@ -498,6 +497,10 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             // next step's block; on the last step the received tag
             dma((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4), b ^ 1);
             step(i, k == 1, raw);
+#ifdef QPP_PROBE
+            if (k == S) QPP_PROBE_AT(8);
+            if (k == S - 1) QPP_PROBE_AT(9);
+#endif
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
@@ -675,28 +678,39 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
     // global access costs microseconds at launch, when every CU issues at once.
     qpp_desc d = {};
     if (valid) d = desc[p];
+#ifdef QPP_PROBE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    QPP_PROBE_AT(10);
+#endif
     if (tid == 0) {
         sm.cur_slot[0] = kNoSlot;
-        sm.base_in = sm.base_out = ~0ull;
     }
     if constexpr (kGcm) load_te<WG>(sm.te);
+#ifdef QPP_PROBE
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    QPP_PROBE_AT(11);
+#endif
     const HdrPre pre = prefetch_hdr<ENC>(d, gin, valid);
+#ifdef QPP_PROBE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    QPP_PROBE_AT(12);
+#endif
     __syncthreads();
+#ifdef QPP_PROBE
+    QPP_PROBE_AT(13);
+#endif
     const uint32_t my_slot = valid ? d.slot : kNoSlot;
     bool done = !valid;
-    if (valid) {
-        atomicMin(&sm.cur_slot[0], my_slot);
-        atomicMin(&sm.base_in, (unsigned long long)d.in_off);
-        atomicMin(&sm.base_out, (unsigned long long)d.out_off);
+    {
+        const uint32_t m = wave_min_u32(my_slot);
+        if (__lane_id() == 0) atomicMin(&sm.cur_slot[0], m);
     }
+    // 32-bit buffer views based at this wave's lowest input / output offsets
+    // (a wave's 16 packets must lie within 4 GiB of each other)
+    const uint64_t bi = wave_min_u64(valid ? d.in_off : ~0ull);
+    const uint64_t bo = wave_min_u64(valid ? d.out_off : ~0ull);
     __syncthreads();
     QPP_PROBE_AT(7);
-    // 32-bit buffer views based at this workgroup's lowest input / output
-    // offsets (a workgroup's packets must lie within 4 GiB of each other)
-    const uint64_t bi = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sm.base_in >> 32)) << 32) |
-                        __builtin_amdgcn_readfirstlane((uint32_t)sm.base_in);
-    const uint64_t bo = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(sm.base_out >> 32)) << 32) |
-                        __builtin_amdgcn_readfirstlane((uint32_t)sm.base_out);
 
     // one iteration per distinct key slot in the workgroup, lowest first;
     // cur_slot is double-buffered so the next minimum is reduced meanwhile
@@ -717,7 +731,10 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
         QPP_PROBE_AT(1);
         const bool in_slot = !done && my_slot == cur;
         done = done || in_slot;
-        if (!done) atomicMin(&sm.cur_slot[(it + 1) & 1], my_slot);
+        {
+            const uint32_t m = wave_min_u32(done ? kNoSlot : my_slot);
+            if (__lane_id() == 0 && m != kNoSlot) atomicMin(&sm.cur_slot[(it + 1) & 1], m);
+        }
         if (in_slot && suite > QPP_CHACHA20_POLY1305 && sub == 0)
             res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
         if (in_slot && mine) {
