@@ -67,8 +67,10 @@ struct KeySlot {
     uint32_t iv[4];      // iv[3] = 0
     uint32_t rk[60];     // AEAD: AES round keys, or the ChaCha20 key in rk[0..7]
     uint32_t hrk[60];    // header protection: AES round keys, or the ChaCha20 HP key
+    uint32_t rkr[60];    // AEAD round keys rotated right by 16 (aes_rounds<.., true>)
+    uint32_t pad[4];
 };
-static_assert(sizeof(KeySlot) == 512, "KeySlot layout");
+static_assert(sizeof(KeySlot) == 768, "KeySlot layout");
 
 // GHASH tables of one slot: [power p = H^(p+1)][window w][nibble v] -> 16 bytes.
 // Window w = 2*byte + (0: low nibble, 1: high nibble).  32 KiB per slot.
@@ -226,6 +228,15 @@ struct LdsTe {
     {
         return rotl(*(const uint32_t *)(te + 128 + addr<3>(s)), 16);
     }
+    // t2 / t3 before their rotation by 16 (rotl16(t2r ^ t3r ^ k') = t2 ^ t3 ^ rotl16(k'))
+    __device__ __forceinline__ uint32_t t2r(uint32_t s) const
+    {
+        return *(const uint32_t *)(te + addr<2>(s));
+    }
+    __device__ __forceinline__ uint32_t t3r(uint32_t s) const
+    {
+        return *(const uint32_t *)(te + 128 + addr<3>(s));
+    }
     // final round: S(x) placed at byte r.  Te0 = (2S,S,S,3S), Te1 = (3S,2S,S,S)
     __device__ __forceinline__ uint32_t f0(uint32_t s) const
     {
@@ -251,6 +262,8 @@ struct ConstTe {
     __device__ __forceinline__ uint32_t t1(uint32_t s) const { return rotl(c_aes.te0[(s >> 8) & 255], 8); }
     __device__ __forceinline__ uint32_t t2(uint32_t s) const { return rotl(c_aes.te0[(s >> 16) & 255], 16); }
     __device__ __forceinline__ uint32_t t3(uint32_t s) const { return rotl(c_aes.te0[s >> 24], 24); }
+    __device__ __forceinline__ uint32_t t2r(uint32_t s) const { return c_aes.te0[(s >> 16) & 255]; }
+    __device__ __forceinline__ uint32_t t3r(uint32_t s) const { return rotl(c_aes.te0[s >> 24], 8); }
     __device__ __forceinline__ uint32_t f0(uint32_t s) const { return c_aes.sbox[s & 255]; }
     __device__ __forceinline__ uint32_t f1(uint32_t s) const { return (uint32_t)c_aes.sbox[(s >> 8) & 255] << 8; }
     __device__ __forceinline__ uint32_t f2(uint32_t s) const { return (uint32_t)c_aes.sbox[(s >> 16) & 255] << 16; }
@@ -260,18 +273,30 @@ struct ConstTe {
 // One AES encryption, state and round keys as little-endian column words.
 // Round: column c takes row r from column c+r (ShiftRows) through Te_r
 // (MixColumns coefficients); the final round substitutes only.
-// Rounds R0..NR on a state that already holds round R0-1's output.
-template <int NR, int R0, class TE>
+// Rounds R0..NR on a state that already holds round R0-1's output.  With
+// KROT the keys of rounds R0..NR-1 are stored rotated right by 16 (KeySlot::
+// rkr) and each column costs 3 VALU besides its lookups:
+//   xor3(T0(a), T1(b), rotl16(xor3(T0(c), T1(d), rotr16(k))))
+// instead of xor3(xor3(T0(a), T1(b), rotl16 T0(c)), rotl16 T1(d), k).
+template <int NR, int R0, bool KROT = false, class TE>
 __device__ __forceinline__ u32x4 aes_rounds(u32x4 st, const uint32_t *rk, const TE &T)
 {
     uint32_t s0 = st.x, s1 = st.y, s2 = st.z, s3 = st.w;
 #pragma unroll
     for (int r = R0; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
-        uint32_t t0 = xor3(xor3(T.t0(s0), T.t1(s1), T.t2(s2)), T.t3(s3), k[0]);
-        uint32_t t1 = xor3(xor3(T.t0(s1), T.t1(s2), T.t2(s3)), T.t3(s0), k[1]);
-        uint32_t t2 = xor3(xor3(T.t0(s2), T.t1(s3), T.t2(s0)), T.t3(s1), k[2]);
-        uint32_t t3 = xor3(xor3(T.t0(s3), T.t1(s0), T.t2(s1)), T.t3(s2), k[3]);
+        uint32_t t0, t1, t2, t3;
+        if constexpr (KROT) {
+            t0 = xor3(T.t0(s0), T.t1(s1), rotl(xor3(T.t2r(s2), T.t3r(s3), k[0]), 16));
+            t1 = xor3(T.t0(s1), T.t1(s2), rotl(xor3(T.t2r(s3), T.t3r(s0), k[1]), 16));
+            t2 = xor3(T.t0(s2), T.t1(s3), rotl(xor3(T.t2r(s0), T.t3r(s1), k[2]), 16));
+            t3 = xor3(T.t0(s3), T.t1(s0), rotl(xor3(T.t2r(s1), T.t3r(s2), k[3]), 16));
+        } else {
+            t0 = xor3(xor3(T.t0(s0), T.t1(s1), T.t2(s2)), T.t3(s3), k[0]);
+            t1 = xor3(xor3(T.t0(s1), T.t1(s2), T.t2(s3)), T.t3(s0), k[1]);
+            t2 = xor3(xor3(T.t0(s2), T.t1(s3), T.t2(s0)), T.t3(s1), k[2]);
+            t3 = xor3(xor3(T.t0(s3), T.t1(s0), T.t2(s1)), T.t3(s2), k[3]);
+        }
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint32_t *k = rk + 4 * NR;
@@ -313,14 +338,15 @@ __device__ __forceinline__ CtrCache ctr_cache(u32x4 nonce, const uint32_t *rk, c
                     xor3(T.t0(u3), T.t2(u1), T.t3(u2)) ^ rk[11]};
 }
 
-// E_K(nonce || BE32(cb)), 1 <= cb < 256, from the packet's cache
+// E_K(nonce || BE32(cb)), 1 <= cb < 256, from the packet's cache.  rk holds
+// plain keys for rounds 0..2 and NR and rotated ones (rkr) for 3..NR-1.
 template <int NR, class TE>
 __device__ __forceinline__ u32x4 aes_ctr(const CtrCache &c, uint32_t cb, const uint32_t *rk,
                                          const TE &T)
 {
     const uint32_t u0 = c.c0 ^ T.t3(rk[3] ^ (cb << 24));
     const u32x4 v = {c.d0 ^ T.t0(u0), c.d1 ^ T.t3(u0), c.d2 ^ T.t2(u0), c.d3 ^ T.t1(u0)};
-    return aes_rounds<NR, 3>(v, rk, T);
+    return aes_rounds<NR, 3, true>(v, rk, T);
 }
 
 // --------------------------------------------------------------- GHASH ----

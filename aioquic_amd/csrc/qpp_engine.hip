@@ -39,6 +39,10 @@ constexpr int kScratch = 96;
 constexpr int kScrTail = 32, kScrEj0 = 48, kScrPark = 64;
 constexpr int kStageBytes = 64 * 16;  // one 16-byte block per lane of a wave
 constexpr uint32_t kNoSlot = 0xffffffffu;
+#ifndef QPP_BALANCE
+#define QPP_BALANCE 1
+#endif
+constexpr bool kBalance = QPP_BALANCE;  // GCM wave balancing (s_setprio)
 
 template <int WG>
 struct __attribute__((aligned(16))) GcmSmem {
@@ -48,6 +52,7 @@ struct __attribute__((aligned(16))) GcmSmem {
     unsigned long long base_in, base_out;
     uint8_t stage[WG / 64][2][kStageBytes];  // per-wave LDS-DMA input staging
     uint32_t cur_slot[2];
+    uint32_t progress;  // steps done by the workgroup's waves (wave balancing)
 };
 
 template <int WG>
@@ -398,7 +403,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                                             const uint8_t *te, const Bufs &B,
                                             const uint8_t *src, uint32_t ioff, uint32_t ooff,
                                             const u32x4 hmask, const uint32_t hbits, const u32x4 h0,
-                                            uint8_t *stage, u32x4 &got_tag)
+                                            uint8_t *stage, uint32_t *progress, u32x4 &got_tag)
 {
     const LdsTe T{te, (uint32_t)(threadIdx.x & 31) * 4};
     const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
@@ -465,7 +470,9 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         // AES and GHASH of a step are independent for unprotect; overlapping
         // them would need more than the 128 VGPRs of 4 waves/SIMD
         __builtin_amdgcn_sched_barrier(0);
-        acc = ghash_mul(acc, lds, last ? (3u - (lane_fresh() & 3)) * 8192u : kTabH4);
+        // H^4 inside the loop (table offset folds into the ds_read immediates);
+        // the last step's H^(4-j) is applied after the loop
+        if (!last) acc = ghash_mul(acc, lds, kTabH4);
     };
     // buffer offset of CT block i's input (or out of range)
     auto ct_load = [&](int i) -> uint32_t {
@@ -490,21 +497,33 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         int i = sub - q, b = 0;
         dma(ct_load(i), 0);
         QPP_PROBE_AT(3);
+        const uint32_t waves = blockDim.x >> 6;
+        uint32_t it = 0;
         for (int k = S; k > 0; --k, i += 4, b ^= 1) {
+            // Wave balancing: issue priority goes to waves behind the
+            // workgroup's average step count (one LDS add per wave and step),
+            // so the waves finish together instead of oldest-first.
+            if (progress) {
+                const uint32_t lane = lane_fresh();
+                uint32_t old = 0;
+                if (lane == __builtin_amdgcn_readfirstlane(lane)) old = atomicAdd(progress, 1u);
+                old = __builtin_amdgcn_readfirstlane(old);
+                if (old > it * waves) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(0);
+                ++it;
+            }
             // the compiler does not track LDS-DMA: retire it explicitly
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const u32x4 raw = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
             // next step's block; on the last step the received tag
             dma((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4), b ^ 1);
             step(i, k == 1, raw);
-#ifdef QPP_PROBE
-            if (k == S) QPP_PROBE_AT(8);
-            if (k == S - 1) QPP_PROBE_AT(9);
-#endif
         }
+        __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
     }
+    acc = ghash_mul(acc, lds, (uint32_t)(3 - sub) * 8192u);
     // the lengths block is the last of the sequence: lane 3, last step
     __builtin_amdgcn_wave_barrier();
     if (sub == 3) acc ^= *(const u32x4 *)(scr + kScrEj0);
@@ -684,6 +703,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
 #endif
     if (tid == 0) {
         sm.cur_slot[0] = kNoSlot;
+        if constexpr (kGcm) sm.progress = 0;
     }
     if constexpr (kGcm) load_te<WG>(sm.te);
 #ifdef QPP_PROBE
@@ -742,10 +762,12 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                 const LdsTe T{sm.te, (uint32_t)(tid & 31) * 4};
                 Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
                 if (P.status == QPP_S_OK) {
+                    // plain keys for rounds 0-2 (counter cache) and NR, rotated between
                     uint32_t rk[4 * (kNR + 1)];
 #pragma unroll
                     for (int i = 0; i < 4 * (kNR + 1); ++i)
-                        rk[i] = __builtin_amdgcn_readfirstlane(ks->rk[i]);
+                        rk[i] = __builtin_amdgcn_readfirstlane(
+                            (i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
                     const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
                     const uint64_t rlen = (uint64_t)(P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN));
                     const uint64_t wlen = (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN);
@@ -765,7 +787,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                             sm.te, B, src, (uint32_t)ioff,
                             (uint32_t)ooff, P.mask, hbits, pre.h0,
                             sm.stage[__builtin_amdgcn_readfirstlane(tid >> 6)][0],
-                            got_tag);
+                            kBalance ? &sm.progress : nullptr, got_tag);
                         QPP_PROBE_AT(4);
                         P = unpark(scr, gin + bi + ioff, gout + bo + ooff, hlen, clen);
                         gcm_finish<ENC, SUITE>(P, ks, sub, scr, T, tag, got_tag);
@@ -858,7 +880,8 @@ __global__ __launch_bounds__(kSetupWG) void k_key_setup(KeySlot *__restrict__ sl
         ks.rsv = 0;
         for (int i = 0; i < 3; ++i) ks.iv[i] = le32(m.iv + 4 * i);
         ks.iv[3] = 0;
-        for (int i = 0; i < 60; ++i) ks.rk[i] = ks.hrk[i] = 0;
+        for (int i = 0; i < 60; ++i) ks.rk[i] = ks.hrk[i] = ks.rkr[i] = 0;
+        for (int i = 0; i < 4; ++i) ks.pad[i] = 0;
         if (m.suite == QPP_CHACHA20_POLY1305) {
             ks.nr = 0;
             for (int i = 0; i < 8; ++i) {
@@ -869,6 +892,7 @@ __global__ __launch_bounds__(kSetupWG) void k_key_setup(KeySlot *__restrict__ sl
             const int klen = m.suite == QPP_AES_256_GCM ? 32 : 16;
             ks.nr = (uint32_t)expand_key(m.key, klen, ks.rk);
             expand_key(m.hp, klen, ks.hrk);
+            for (int i = 0; i < 60; ++i) ks.rkr[i] = rotl(ks.rk[i], 16);
             const ConstTe CT;
             const u32x4 zero = {0, 0, 0, 0};
             const u32x4 h = ks.nr == 14 ? aes_encrypt<14>(zero, ks.rk, CT)

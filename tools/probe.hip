@@ -22,10 +22,9 @@ static void fill(uint8_t *p, size_t n, uint32_t seed)
 static void report(const char *what, const std::vector<unsigned long long> &pr, int waves)
 {
     const char *names[] = {"  desc load", "  load_te", "  hdr prefetch", "  sync 1", "  atomics + sync 2", "prologue (te, desc, hdr, 2 syncs)", "slot + GHASH table", "pkt_begin",
-                           "AAD fold + ctr cache", "step loop", "  first step", "  second step",
-                           "  remaining steps", "finish + result", "final sync"};
-    const int from[] = {0, 10, 11, 12, 13, 0, 7, 1, 2, 3, 3, 8, 9, 4, 5}, to[] = {10, 11, 12, 13, 7, 7, 1, 2, 3, 4, 8, 9, 4, 5, 6};
-    constexpr int NP = 15;
+                           "AAD fold + ctr cache", "step loop", "finish + result", "final sync"};
+    const int from[] = {0, 10, 11, 12, 13, 0, 7, 1, 2, 3, 4, 5}, to[] = {10, 11, 12, 13, 7, 7, 1, 2, 3, 4, 5, 6};
+    constexpr int NP = 12;
     unsigned long long t0 = ~0ull, t1 = 0;
     for (int w = 0; w < waves; ++w) {
         t0 = std::min(t0, pr[w * 16 + 0]);
