@@ -46,14 +46,35 @@ constexpr bool kBalance = QPP_BALANCE;  // GCM wave balancing (s_setprio)
 
 template <int WG>
 struct __attribute__((aligned(16))) GcmSmem {
-    uint8_t te[kTeBytes];             // Te0|Te1 x 32 bank copies   64 KiB
+    // GHASH tables first: every table offset (< 32 KiB) and the AES image
+    // base (32 KiB) then fit the 16-bit ds_read immediate
     uint8_t gt[kGhashTabBytes];       // GHASH H^1..H^4 tables      32 KiB
+    uint8_t te[kTeBytes];             // Te0|Te1 x 32 bank copies   64 KiB
     uint8_t scratch[WG / 4][kScratch];
-    unsigned long long base_in, base_out;
     uint8_t stage[WG / 64][2][kStageBytes];  // per-wave LDS-DMA input staging
+    KeySlot kslot;                           // the current key slot (LDS-DMA)
     uint32_t cur_slot[2];
     uint32_t progress;  // steps done by the workgroup's waves (wave balancing)
 };
+
+// LDS-DMA of key slot s (768 B) and its GHASH tables (32 KiB) into a GCM
+// workgroup's LDS: one 1 KiB chunk per wave instruction.  The caller retires
+// it with s_waitcnt vmcnt(0) before the barrier that precedes any use.
+template <int WG>
+__device__ __forceinline__ void stage_key(GcmSmem<WG> &sm, const KeySlot *slots,
+                                          const uint8_t *gtab, uint32_t s)
+{
+    typedef const __attribute__((address_space(1))) void *gptr_t;
+    typedef __attribute__((address_space(3))) void *lptr_t;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint8_t *gt = gtab + (size_t)s * kGhashTabBytes;
+    for (int c = w; c < kGhashTabBytes / 1024; c += WG / 64)
+        __builtin_amdgcn_global_load_lds((gptr_t)(gt + c * 1024 + l * 16), (lptr_t)(sm.gt + c * 1024),
+                                         16, 0, 0);
+    if (w == 0 && l < (int)(sizeof(KeySlot) / 16))
+        __builtin_amdgcn_global_load_lds((gptr_t)((const uint8_t *)(slots + s) + l * 16),
+                                         (lptr_t)&sm.kslot, 16, 0, 0);
+}
 
 template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
@@ -705,7 +726,17 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
         sm.cur_slot[0] = kNoSlot;
         if constexpr (kGcm) sm.progress = 0;
     }
-    if constexpr (kGcm) load_te<WG>(sm.te);
+    // key material: speculate that the workgroup's packets use the slot of
+    // its first packet (host batches are grouped by slot) and stage it now
+    uint32_t staged = kNoSlot;
+    if constexpr (kGcm) {
+        const uint32_t spec = __builtin_amdgcn_readfirstlane(desc[blockIdx.x * kPktPerWG].slot);
+        if (spec < cap) {
+            stage_key<WG>(sm, slots, gtab, spec);
+            staged = spec;
+        }
+        load_te<WG>(sm.te);
+    }
 #ifdef QPP_PROBE
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     QPP_PROBE_AT(11);
@@ -715,6 +746,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     QPP_PROBE_AT(12);
 #endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged key slot (LDS-DMA)
     __syncthreads();
 #ifdef QPP_PROBE
     QPP_PROBE_AT(13);
@@ -737,17 +769,21 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
     for (int it = 0;; ++it) {
         const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur_slot[it & 1]);
         if (cur == kNoSlot) break;
-        const KeySlot *ks = slots + cur;
-        const uint32_t suite = cur < cap ? ks->suite : 0xffu;
-        const bool mine = suite == SUITE;
-        if (tid == 0) sm.cur_slot[(it + 1) & 1] = kNoSlot;
         if constexpr (kGcm) {
-            if (mine) {
-                const u32x4 *src = (const u32x4 *)(gtab + (size_t)cur * kGhashTabBytes);
-                for (int i = tid; i < kGhashTabBytes / 16; i += WG) ((u32x4 *)sm.gt)[i] = src[i];
+            if (cur != staged) {  // the speculation missed, or a further slot
+                if (cur < cap) stage_key<WG>(sm, slots, gtab, cur);
+                staged = cur;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
+        if (tid == 0) sm.cur_slot[(it + 1) & 1] = kNoSlot;
         __syncthreads();
+        // GCM reads its key material from the staged LDS copy
+        const KeySlot *ks;
+        if constexpr (kGcm) ks = &sm.kslot;
+        else ks = slots + cur;
+        const uint32_t suite = cur < cap ? ks->suite : 0xffu;
+        const bool mine = suite == SUITE;
         QPP_PROBE_AT(1);
         const bool in_slot = !done && my_slot == cur;
         done = done || in_slot;
@@ -759,6 +795,12 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
             res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
         if (in_slot && mine) {
             if constexpr (kGcm) {
+                // Re-read the descriptor and header words (L2 hits: the
+                // prologue fetched them) so that neither stays live through
+                // the step loop, where 128 VGPRs leave no room for them.
+                asm volatile("" ::: "memory");
+                const qpp_desc d = desc[p];
+                const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
                 const LdsTe T{sm.te, (uint32_t)(tid & 31) * 4};
                 Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
                 if (P.status == QPP_S_OK) {
@@ -787,7 +829,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                             sm.te, B, src, (uint32_t)ioff,
                             (uint32_t)ooff, P.mask, hbits, pre.h0,
                             sm.stage[__builtin_amdgcn_readfirstlane(tid >> 6)][0],
-                            kBalance ? &sm.progress : nullptr, got_tag);
+                            (kBalance && !ENC) ? &sm.progress : nullptr, got_tag);
                         QPP_PROBE_AT(4);
                         P = unpark(scr, gin + bi + ioff, gout + bo + ooff, hlen, clen);
                         gcm_finish<ENC, SUITE>(P, ks, sub, scr, T, tag, got_tag);

@@ -89,6 +89,30 @@ int main(int argc, char **argv)
     (void)hipMemcpy(d_pd, pd.data(), n * sizeof(qpp_desc), hipMemcpyHostToDevice);
     (void)hipMemcpy(d_ud, ud.data(), n * sizeof(qpp_desc), hipMemcpyHostToDevice);
 
+    if (argc > 3 && strcmp(argv[3], "bench") == 0) {
+        // bench.py's step: protect then unprotect, alternating, event-timed
+        const int steps = 30;
+        hipEvent_t ev[3];
+        for (auto &e : ev) (void)hipEventCreate(&e);
+        double tp = 0, tu = 0;
+        for (int k = -5; k < steps; ++k) {
+            (void)hipEventRecord(ev[0], nullptr);
+            (void)qpp_protect(kt, d_pd, n, d_in, d_ct, d_res, nullptr);
+            (void)hipEventRecord(ev[1], nullptr);
+            (void)qpp_unprotect(kt, d_ud, n, d_ct, d_pt, d_res, nullptr);
+            (void)hipEventRecord(ev[2], nullptr);
+            (void)hipEventSynchronize(ev[2]);
+            float a = 0, b = 0;
+            (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+            (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+            if (k >= 0) { tp += a; tu += b; }
+        }
+        tp /= steps;
+        tu /= steps;
+        printf("bench: protect %.1f us unprotect %.1f us -> %.1f GiB/s\n", tp * 1e3, tu * 1e3,
+               (double)n * 1200 / ((tp + tu) * 1e-3) / (1u << 30));
+        return 0;
+    }
     const int wg = suite == QPP_CHACHA20_POLY1305 ? wg_choice("QPP_WG_CHACHA", kChachaWG)
                                                   : wg_choice("QPP_WG_GCM", kGcmWG);
     const int waves = (int)(((n + wg / 4 - 1) / (wg / 4)) * (wg / 64));
