@@ -365,8 +365,11 @@ __device__ __forceinline__ u32x4 ghash_mul(u32x4 x, const uint8_t *lds, uint32_t
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const int wlo = 2 * (4 * d + b), whi = wlo + 1;
-            uint32_t alo = __builtin_amdgcn_ubfe(lo, 8 * b, 8);
-            uint32_t ahi = __builtin_amdgcn_ubfe(hi, 8 * b, 8);
+            // byte b of the pre-masked nibble words, zero-extended: one v_perm
+            // each (ubfe gets rewritten into shift + mask, two ops)
+            const uint32_t sel = 0x0c0c0c00u | (uint32_t)b;
+            uint32_t alo = __builtin_amdgcn_perm(0u, lo, sel);
+            uint32_t ahi = __builtin_amdgcn_perm(0u, hi, sel);
             u32x4 e0 = *(const u32x4 *)(lds + tab + wlo * 256 + alo);
             u32x4 e1 = *(const u32x4 *)(lds + tab + whi * 256 + ahi);
             acc = xor3(acc, e0, e1);

@@ -34,9 +34,10 @@ __constant__ AesTables c_aes = kAesTables;
 constexpr int kSetupWG = 256;
 // Per-packet LDS scratch: [0, 32) ct[0..32) (+ tag) for the protect HP
 // sample; [32, 48) tiny-input staging, then the partial tail block; [48, 64)
-// E_K(J0); [64, 96) the parked packet view (GCM step loop).
-constexpr int kScratch = 96;
-constexpr int kScrTail = 32, kScrEj0 = 48, kScrPark = 64;
+// E_K(J0); [64, 96) the parked packet view (GCM step loop); [96, 112) input
+// bytes [0, 16) (the first header block) for the header write.
+constexpr int kScratch = 112;
+constexpr int kScrTail = 32, kScrEj0 = 48, kScrPark = 64, kScrHdr = 96;
 constexpr int kStageBytes = 64 * 16;  // one 16-byte block per lane of a wave
 constexpr uint32_t kNoSlot = 0xffffffffu;
 #ifndef QPP_BALANCE
@@ -283,7 +284,8 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const HdrPre &pre, c
 // Protect: header protection over the finished (ct||tag) and the header write.
 template <int SUITE, class TE>
 __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int sub,
-                                                  uint8_t *scr, u32x4 tag, const TE &T)
+                                                  uint8_t *scr, u32x4 tag, const TE &T,
+                                                  const uint8_t *h0 = nullptr)
 {
     // sample = (ct||tag)[4-pn_len : 20-pn_len]; the tag only matters when clen < 20
     if (P.clen < 32 && sub == 0) {
@@ -296,7 +298,7 @@ __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int
     const int n_a = (P.hlen + 15) >> 4;
     for (int q = sub; q < n_a; q += 4) {
         const int nb = min(16, P.hlen - 16 * q);
-        u32x4 h = ld_part(P.src + 16 * q, nb);
+        u32x4 h = (q == 0 && h0) ? *(const u32x4 *)h0 : ld_part(P.src + 16 * q, nb);
         h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
         st_part(P.dst + 16 * q, h, nb);
     }
@@ -304,12 +306,14 @@ __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int
 
 // Header out: the plain header (unprotect), or the input header with the HP
 // mask applied (protect).  Outside the step loop; byte tails allowed here.
-__device__ __forceinline__ void write_header(const Pkt &P, int sub, bool masked)
+// h0: the input's first 16 bytes already in LDS (or null: read them).
+__device__ __forceinline__ void write_header(const Pkt &P, int sub, bool masked,
+                                             const uint8_t *h0 = nullptr)
 {
     const int n_a = (P.hlen + 15) >> 4;
     for (int q = sub; q < n_a; q += 4) {
         const int nb = min(16, P.hlen - 16 * q);
-        u32x4 h = ld_part(P.src + 16 * q, nb);
+        u32x4 h = (q == 0 && h0) ? *(const u32x4 *)h0 : ld_part(P.src + 16 * q, nb);
         if (masked) h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
         st_part(P.dst + 16 * q, h, nb);
     }
@@ -561,14 +565,16 @@ __device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, u
     const int n_g = za + n_c + 1, pad = 4 * ((n_g + 3) >> 2) - n_g;
     if ((P.clen & 15) && sub == ((pad + za + n_c - 1) & 3))
         st_part(P.dst + P.hlen + 16 * (n_c - 1), *(const u32x4 *)(scr + kScrTail), P.clen & 15);
+    // input bytes [0, 16) parked in LDS by the prologue (absent for tiny input)
+    const uint8_t *h0 = (P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN) >= 16) ? scr + kScrHdr : nullptr;
     if (ENC) {
         if (sub == 0) st16(P.dst + P.hlen + P.clen, tag);
-        if (P.hp) protect_finish_hp<SUITE>(P, ks, sub, scr, tag, T);
-        else write_header(P, sub, false);
+        if (P.hp) protect_finish_hp<SUITE>(P, ks, sub, scr, tag, T, h0);
+        else write_header(P, sub, false, h0);
     } else {
         const u32x4 diff = got_tag ^ tag;
         if ((diff.x | diff.y | diff.z | diff.w) != 0) P.status = QPP_S_DECRYPT;
-        write_header(P, sub, P.hp);
+        write_header(P, sub, P.hp, h0);
     }
 }
 
@@ -822,6 +828,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                         const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 |
                                                (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28;
                         park(P, scr);
+                        *(u32x4 *)(scr + kScrHdr) = pre.h0;
                         QPP_PROBE_AT(2);
                         u32x4 got_tag;
                         const u32x4 tag = gcm_packet<kNR, ENC>(

@@ -117,12 +117,13 @@ int main(int argc, char **argv)
                                                   : wg_choice("QPP_WG_GCM", kGcmWG);
     const int waves = (int)(((n + wg / 4 - 1) / (wg / 4)) * (wg / 64));
     std::vector<unsigned long long> pr((size_t)waves * 16);
+    // warm up in bench.py's order (protect, unprotect alternating)
+    for (int rep = 0; rep < 3; ++rep) {
+        int rc = qpp_protect(kt, d_pd, n, d_in, d_ct, d_res, nullptr);
+        rc |= qpp_unprotect(kt, d_ud, n, d_ct, d_pt, d_res, nullptr);
+        if (rc != QPP_OK) { printf("launch rc %d\n", rc); return 1; }
+    }
     for (int enc = 1; enc >= 0; --enc) {
-        for (int rep = 0; rep < 3; ++rep) {
-            int rc = enc ? qpp_protect(kt, d_pd, n, d_in, d_ct, d_res, nullptr)
-                         : qpp_unprotect(kt, d_ud, n, d_ct, d_pt, d_res, nullptr);
-            if (rc != QPP_OK) { printf("launch rc %d\n", rc); return 1; }
-        }
         hipEvent_t a, b;
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
