@@ -143,12 +143,14 @@ def main():
     from aioquic_amd import layout as L
     from aioquic_amd.batch import PacketEngine
     from aioquic_amd.bench_data import make_workload
+    from aioquic_amd.shard import shard_range
 
     cfg = CONFIGS[args.config]
     n = args.packets or cfg["n"]
     # shard: rank r owns packets [r*n, (r+1)*n) of the global stream
+    first, n = shard_range(rank, world, n)
     w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=0x9001 + args.config,
-                      version=cfg["version"], mixed=cfg.get("mixed"), first_packet=rank * n)
+                      version=cfg["version"], mixed=cfg.get("mixed"), first_packet=first)
     eng = PacketEngine(w.n_keys)
     eng.set_key_records(w.keys)
 
@@ -278,7 +280,17 @@ def e2e(eng, w, dev, n, chunks=8, reps=5):
         torch.cuda.synchronize(dev)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
+    # the PCIe legs alone, same buffers (what bounds the host-resident rate)
+    leg = {}
+    for name, dst, src in (("h2d", d_in, h_in), ("d2h", h_out, d_out)):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        leg[name] = round(reps * src.numel() / (time.perf_counter() - t0) / GIB, 3)
     return {"gib_s": round(per * chunks * 1200 / t / GIB, 3), "chunks": chunks,
+            "h2d_gib_s": leg["h2d"], "d2h_gib_s": leg["d2h"],
             "note": "pinned H2D + protect + unprotect + D2H, 2 streams"}
 
 
