@@ -278,7 +278,8 @@ static PyObject *HP_apply(HPObject *self, PyObject *args)
     }
     int pn_len = (hdr[0] & 3) + 1;
     Py_ssize_t pn_off = hlen - pn_len;
-    if (pn_off < 0 || plen < 20 - pn_len) {
+    /* hlen + plen > 1500 overruns the reference's buffer (_crypto.c:305-306) */
+    if (pn_off < 0 || plen < 20 - pn_len || hlen + plen > QPP_PACKET_MAX) {
         PyErr_SetString(g_crypto_error, "Invalid payload length");
         return NULL;
     }

@@ -242,7 +242,12 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const HdrPre &pre, c
                 P.pn_len = (int)(b0 & 3) + 1;
                 P.pn_off = P.hlen - P.pn_len;
                 P.fbm = first_byte_mask(b0);
-                if (P.pn_off < 0 || P.clen + QPP_TAG_LEN < 20 - P.pn_len) P.status = QPP_S_LENGTH;
+                // defined domain of the reference: AEAD.encrypt output fits
+                // buffer[1500] (_crypto.c:168-171,193) and apply's header ||
+                // payload copy fits buffer[1500] (_crypto.c:305-306)
+                if (P.pn_off < 0 || P.clen + QPP_TAG_LEN < 20 - P.pn_len ||
+                    P.hlen + P.clen + QPP_TAG_LEN > QPP_PACKET_MAX)
+                    P.status = QPP_S_LENGTH;
             }
         }
     } else if (P.hp) {

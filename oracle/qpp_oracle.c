@@ -462,7 +462,10 @@ long qo_protect(int suite, const uint8_t *key, const uint8_t iv[12], const uint8
                 const uint8_t *hdr, size_t hlen, const uint8_t *payload, size_t plen,
                 uint64_t pn, uint8_t *out)
 {
-    if (plen > QO_PACKET_MAX - 16) return -1;
+    /* the reference's defined domain: AEAD.encrypt's output fits buffer[1500]
+     * (_crypto.c:168-171,193) and HeaderProtection.apply copies header ||
+     * payload into buffer[1500] (_crypto.c:305-306); beyond that it overruns */
+    if (plen > QO_PACKET_MAX - 16 || hlen + plen + 16 > QO_PACKET_MAX) return -1;
     long n = qo_aead_encrypt(suite, key, iv, payload, plen, hdr, hlen, pn, out + hlen);
     if (n < 0) return -1;
     if (qo_hp_apply(suite, hp_key, hdr, hlen, out + hlen, (size_t)n, out) != 0) return -1;

@@ -65,7 +65,7 @@ def test_send_batch_matches_per_packet_and_oracle(oracle):
         if rng.random() < 0.02:  # a local key update between packets (crypto.py:194-199)
             cl.update_key()
             cl2.update_key()
-        pl = int(rng.choice([1, 4, 20, 300, 1173, 1400]))
+        pl = int(rng.choice([4, 5, 20, 300, 1173, 1400]))  # >= 4: the HP sample must exist
         hdr = _short_header(cl.key_phase, pn[j], pn_len=int(rng.integers(1, 5)))
         payload = rng.bytes(pl)
         batch.add(cl, hdr, payload, pn[j])
@@ -89,7 +89,7 @@ def test_send_batch_rejects_like_reference():
     (cl, _), _ = _pairs(rng, "AES_128_GCM_SHA256")
     b = SendBatch(capacity=4)
     b.add(cl, _short_header(0, 1), b"x" * 100, 1)
-    b.add(cl, _short_header(0, 2), b"x" * 1490, 2)  # hdr + payload > 1500: undefined in the reference
+    b.add(cl, _short_header(0, 2), b"x" * 1474, 2)  # 11 + 1474 + 16 > 1500: overruns the reference
     with pytest.raises(CryptoError, match="Invalid payload length"):
         b.flush()
 
@@ -182,7 +182,7 @@ def test_receive_batch_many_connections():
     for k, (cl, sv) in enumerate(conns):
         for pn in range(3):
             hdr = _short_header(0, pn, pn_len=1 + (k % 4))
-            payload = rng.bytes(int(rng.integers(1, 1173)))
+            payload = rng.bytes(int(rng.integers(4, 1173)))
             sb.add(cl, hdr, payload, pn)
             meta.append((sv, 9, pn, hdr, payload))
     wires = sb.flush()

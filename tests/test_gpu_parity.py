@@ -416,3 +416,46 @@ def test_in_place(oracle, L, engine_cls):
     for i in range(256):
         o, n = int(desc[i]["out_off"]), len(headers[i]) + len(payloads[i]) + 16
         assert np.array_equal(got[o : o + n], exp[o : o + n])
+
+
+def test_fused_protect_length_boundary(oracle, L, engine_cls):
+    """hdr + payload + tag = 1500 is the last defined size of the reference's
+    encrypt_packet (buffer[1500], _crypto.c:168-171,305-306); one byte more is
+    "Invalid payload length" in the kernel, the oracle and the object API."""
+    import torch
+
+    from aioquic_amd._crypto import CryptoError, HeaderProtection
+    from aioquic_amd.batch import layout_packets
+
+    rng = np.random.default_rng(13)
+    recs = _keys(rng, 3)
+    eng = engine_cls(3)
+    eng.set_key_records(recs)
+    headers, payloads, slots = [], [], []
+    for s in range(3):
+        for hl, extra in ((11, 0), (11, 1), (40, 0), (40, 1), (5, 0)):
+            headers.append(short_header(rng.bytes(hl - 3), s, 2, 0))
+            payloads.append(rng.bytes(1500 - 16 - hl + extra))
+            slots.append(s)
+    n = len(headers)
+    inbuf, desc, size = layout_packets(headers, payloads, list(range(n)), slots)
+    exp, eres = oracle.protect_batch(recs, desc, inbuf, size)
+    d_in = torch.from_numpy(inbuf).cuda()
+    d_out = torch.zeros(size, dtype=torch.uint8, device="cuda")
+    d = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
+    res = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    eng.protect(d, n, d_in, d_out, res)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(L.RESULT)
+    assert list(r["status"]) == list(eres["status"])
+    want = [0 if len(h) + len(p) + 16 <= 1500 else L.S_LENGTH for h, p in zip(headers, payloads)]
+    assert list(r["status"]) == want
+    got = d_out.cpu().numpy()
+    for i in range(n):
+        if want[i] == 0:
+            o, m = int(desc[i]["out_off"]), int(r[i]["out_len"])
+            assert np.array_equal(got[o : o + m], exp[o : o + m])
+    hp = HeaderProtection(b"aes-128-ecb", bytes(16))
+    assert len(hp.apply(b"\x40" + bytes(10), bytes(1489))) == 1500
+    with pytest.raises(CryptoError, match="Invalid payload length"):
+        hp.apply(b"\x40" + bytes(10), bytes(1490))
