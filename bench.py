@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--e2e", action="store_true", help="also time pinned H2D->kernels->D2H")
+    ap.add_argument("--e2e-chunks", type=int, default=16)
+    ap.add_argument("--e2e-streams", type=int, default=4)
     ap.add_argument("--check", action="store_true", help="verify round trip after timing")
     return ap.parse_args()
 
@@ -238,16 +240,17 @@ def main():
             "status_ok": ok,
         }
         if args.e2e:
-            out["e2e"] = e2e(eng, w, dev, n)
+            out["e2e"] = e2e(eng, w, dev, n, chunks=args.e2e_chunks, n_streams=args.e2e_streams)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def e2e(eng, w, dev, n, chunks=8, reps=5):
-    """Pinned host -> H2D -> protect -> unprotect -> D2H, pipelined over two
-    streams in `chunks` slices (the path starts and ends in UDP socket buffers)."""
+def e2e(eng, w, dev, n, chunks=16, n_streams=4, reps=5):
+    """Pinned host -> H2D -> protect -> unprotect -> D2H, pipelined over
+    `n_streams` streams in `chunks` slices (the path starts and ends in UDP
+    socket buffers)."""
     import torch
 
     h_in = torch.from_numpy(w.plain).pin_memory()
@@ -256,7 +259,7 @@ def e2e(eng, w, dev, n, chunks=8, reps=5):
     d_wire = torch.empty(w.wire_size, dtype=torch.uint8, device=dev)
     d_out = torch.empty(w.plain_size, dtype=torch.uint8, device=dev)
     per = n // chunks
-    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
     descs, udescs, res = [], [], []
     for c in range(chunks):
         d = w.desc[c * per : (c + 1) * per].copy()
@@ -270,7 +273,7 @@ def e2e(eng, w, dev, n, chunks=8, reps=5):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for c in range(chunks):
-            s = streams[c % 2]
+            s = streams[c % n_streams]
             with torch.cuda.stream(s):
                 lo, hi = c * span, (c + 1) * span
                 d_in[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
@@ -289,9 +292,20 @@ def e2e(eng, w, dev, n, chunks=8, reps=5):
             dst.copy_(src, non_blocking=True)
         torch.cuda.synchronize(dev)
         leg[name] = round(reps * src.numel() / (time.perf_counter() - t0) / GIB, 3)
+    # both directions at once on two streams (the duplex bound of the link)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        with torch.cuda.stream(streams[0]):
+            d_in.copy_(h_in, non_blocking=True)
+        with torch.cuda.stream(streams[1 % n_streams]):
+            h_out.copy_(d_out, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    leg["duplex"] = round(reps * h_in.numel() / (time.perf_counter() - t0) / GIB, 3)
     return {"gib_s": round(per * chunks * 1200 / t / GIB, 3), "chunks": chunks,
-            "h2d_gib_s": leg["h2d"], "d2h_gib_s": leg["d2h"],
-            "note": "pinned H2D + protect + unprotect + D2H, 2 streams"}
+            "streams": n_streams, "h2d_gib_s": leg["h2d"], "d2h_gib_s": leg["d2h"],
+            "duplex_gib_s_each_way": leg["duplex"],
+            "note": f"pinned H2D + protect + unprotect + D2H, {n_streams} streams"}
 
 
 if __name__ == "__main__":
