@@ -59,6 +59,13 @@ class PacketEngine:
         )
         self.table.set(recs.tobytes())
 
+    def derive_keys(self, secrets: np.ndarray) -> np.ndarray:
+        """Batched CryptoContext.setup on the device (qpp_keytab_derive):
+        `secrets` are layout.SECRET records; returns the derived KEY_MATERIAL."""
+        assert secrets.dtype == L.SECRET
+        km = self.table.derive(np.ascontiguousarray(secrets).tobytes())
+        return np.frombuffer(km, dtype=L.KEY_MATERIAL).copy()
+
     def set_key_records(self, recs: np.ndarray) -> None:
         assert recs.dtype == L.KEY_MATERIAL
         self.table.set(np.ascontiguousarray(recs).tobytes())

@@ -21,7 +21,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 HIP_SOURCES = ["qpp_engine.hip"]
-HIP_DEPS = HIP_SOURCES + ["qpp_device.h", "qpp_chacha.h"]
+HIP_DEPS = HIP_SOURCES + ["qpp_device.h", "qpp_chacha.h", "qpp_hkdf.h", "qpp_sha_consts.h"]
 
 
 def _stale(target, deps):

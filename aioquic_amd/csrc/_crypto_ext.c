@@ -401,6 +401,42 @@ static PyObject *KT_set(KeyTableObject *self, PyObject *args)
     Py_RETURN_NONE;
 }
 
+/* KeyTable.derive(secrets) -> key material: batched CryptoContext.setup
+ * (qpp_keytab_derive); secrets = whole qpp_secret records. */
+static PyObject *KT_derive(KeyTableObject *self, PyObject *args)
+{
+    Py_buffer b;
+    unsigned long long stream = 0;
+    if (!PyArg_ParseTuple(args, "y*|K", &b, &stream)) return NULL;
+    if (b.len % (Py_ssize_t)sizeof(qpp_secret)) {
+        PyBuffer_Release(&b);
+        PyErr_SetString(PyExc_ValueError, "secrets must be a whole number of 80-byte records");
+        return NULL;
+    }
+    uint32_t n = (uint32_t)(b.len / (Py_ssize_t)sizeof(qpp_secret));
+    PyObject *km = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_key_material));
+    if (!km) {
+        PyBuffer_Release(&b);
+        return NULL;
+    }
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = qpp_keytab_derive(self->kt, (const qpp_secret *)b.buf, n,
+                           (qpp_key_material *)PyBytes_AS_STRING(km), (void *)(uintptr_t)stream);
+    Py_END_ALLOW_THREADS
+    PyBuffer_Release(&b);
+    if (rc == QPP_E_ARG) {
+        Py_DECREF(km);
+        PyErr_SetString(PyExc_ValueError, "bad secret (slot out of range, unknown suite or length)");
+        return NULL;
+    }
+    if (check_rc(rc) < 0) {
+        Py_DECREF(km);
+        return NULL;
+    }
+    return km;
+}
+
 static PyObject *KT_clear(KeyTableObject *self, PyObject *args)
 {
     Py_buffer b;
@@ -419,6 +455,7 @@ static PyObject *KT_capacity(KeyTableObject *self, void *unused)
 static PyMethodDef KT_methods[] = {
     {"set", (PyCFunction)KT_set, METH_VARARGS, "set(materials, stream=0)"},
     {"clear", (PyCFunction)KT_clear, METH_VARARGS, "clear(slots_u32)"},
+    {"derive", (PyCFunction)KT_derive, METH_VARARGS, "derive(secrets, stream=0) -> key material"},
     {NULL},
 };
 

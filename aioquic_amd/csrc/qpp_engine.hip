@@ -22,6 +22,7 @@
 
 #include "qpp_chacha.h"
 #include "qpp_device.h"
+#include "qpp_hkdf.h"
 
 namespace qpp {
 
@@ -972,6 +973,47 @@ __global__ __launch_bounds__(kSetupWG) void k_key_setup(KeySlot *__restrict__ sl
     }
 }
 
+// Batched derive_key_iv_hp (quic/crypto.py:34-56), one lane per connection:
+// `updates` x "quic ku" (next_key_phase, :157-168), then key / iv / hp by
+// HKDF-Expand-Label with the v1 or v2 labels.  Cold path (once per key).
+constexpr int kDeriveWG = 64;
+
+__global__ __launch_bounds__(kDeriveWG) void k_derive(const qpp_secret *__restrict__ sec,
+                                                      uint32_t n,
+                                                      qpp_key_material *__restrict__ km)
+{
+    const uint32_t i = blockIdx.x * kDeriveWG + threadIdx.x;
+    if (i >= n) return;
+    const qpp_secret &s = sec[i];
+    const bool big = s.suite == QPP_AES_256_GCM;
+    const int hl = big ? 48 : 32, klen = s.suite == QPP_AES_128_GCM ? 16 : 32;
+    uint8_t secret[64];
+    int len = s.secret_len;
+    for (int j = 0; j < 64; ++j) secret[j] = j < len ? s.secret[j] : 0;
+    qpp_hkdf::Hmac m;
+    for (uint32_t u = 0; u < s.updates; ++u) {
+        qpp_hkdf::hmac_init(m, big, secret, len);
+        qpp_hkdf::expand_label(m, "quic ku", 7, hl, secret);
+        len = hl;
+    }
+    qpp_hkdf::hmac_init(m, big, secret, len);
+    qpp_key_material r;
+    memset(&r, 0, sizeof(r));
+    r.slot = s.slot;
+    r.suite = s.suite;
+    r.key_phase = s.key_phase & 1;
+    if (s.flags & QPP_DERIVE_V2) {
+        qpp_hkdf::expand_label(m, "quicv2 key", 10, klen, r.key);
+        qpp_hkdf::expand_label(m, "quicv2 iv", 9, 12, r.iv);
+        qpp_hkdf::expand_label(m, "quicv2 hp", 9, klen, r.hp);
+    } else {
+        qpp_hkdf::expand_label(m, "quic key", 8, klen, r.key);
+        qpp_hkdf::expand_label(m, "quic iv", 7, 12, r.iv);
+        qpp_hkdf::expand_label(m, "quic hp", 7, klen, r.hp);
+    }
+    km[i] = r;
+}
+
 __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, uint32_t cap)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1100,6 +1142,47 @@ int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void 
     // key material is host memory owned by the caller: finish before returning
     HIPCHK(hipStreamSynchronize(s));
     return QPP_OK;
+}
+
+int qpp_keytab_derive(qpp_keytab *kt, const qpp_secret *sec, uint32_t n,
+                      qpp_key_material *km_out, void *stream)
+{
+    if (!kt || (!sec && n)) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (sec[i].slot >= kt->cap || sec[i].suite > QPP_CHACHA20_POLY1305 ||
+            sec[i].secret_len < 1 || sec[i].secret_len > 64)
+            return QPP_E_ARG;
+    for (uint32_t i = 0; i < n; ++i) kt->suite_mask |= 1u << sec[i].suite;
+    hipStream_t s = (hipStream_t)stream;
+    if (n > kt->km_cap) {
+        if (kt->d_km) HIPCHK(hipFree(kt->d_km));
+        kt->d_km = NULL;
+        kt->km_cap = 0;
+        HIPCHK(hipMalloc(&kt->d_km, (size_t)n * sizeof(qpp_key_material)));
+        kt->km_cap = n;
+    }
+    qpp_secret *d_sec = NULL;
+    HIPCHK(hipMalloc(&d_sec, (size_t)n * sizeof(qpp_secret)));
+    int rc = QPP_OK;
+    if (hipMemcpyAsync(d_sec, sec, (size_t)n * sizeof(qpp_secret), hipMemcpyHostToDevice, s) !=
+        hipSuccess) {
+        rc = QPP_E_HIP;
+    } else {
+        hipLaunchKernelGGL(k_derive, dim3((n + kDeriveWG - 1) / kDeriveWG), dim3(kDeriveWG), 0, s,
+                           d_sec, n, kt->d_km);
+        hipLaunchKernelGGL(k_key_setup, dim3(n), dim3(kSetupWG), 0, s, kt->d_slots, kt->d_gtab,
+                           kt->cap, kt->d_km, n);
+        if (hipGetLastError() != hipSuccess) rc = QPP_E_HIP;
+        else if (km_out && hipMemcpyAsync(km_out, kt->d_km, (size_t)n * sizeof(qpp_key_material),
+                                          hipMemcpyDeviceToHost, s) != hipSuccess)
+            rc = QPP_E_HIP;
+    }
+    // the secrets are caller host memory: finish before returning
+    if (hipStreamSynchronize(s) != hipSuccess && rc == QPP_OK) rc = QPP_E_HIP;
+    (void)hipFree(d_sec);
+    (void)hipGetLastError();
+    return rc;
 }
 
 int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *stream)

@@ -37,7 +37,21 @@ KEY_MATERIAL = np.dtype(
         ("hp", "u1", (32,)),
     ]
 )
+SECRET = np.dtype(
+    [
+        ("slot", "<u4"),
+        ("suite", "u1"),
+        ("key_phase", "u1"),
+        ("flags", "u1"),
+        ("secret_len", "u1"),
+        ("updates", "<u4"),
+        ("rsv", "<u4"),
+        ("secret", "u1", (64,)),
+    ]
+)
+DERIVE_V2 = 1
 assert DESC.itemsize == 40 and RESULT.itemsize == 16 and KEY_MATERIAL.itemsize == 84
+assert SECRET.itemsize == 80
 
 
 def key_material(slot: int, suite: int, key: bytes, iv: bytes, hp: bytes, key_phase: int = 0):
@@ -48,4 +62,20 @@ def key_material(slot: int, suite: int, key: bytes, iv: bytes, hp: bytes, key_ph
     rec["iv"][0, : len(iv)] = np.frombuffer(iv, dtype=np.uint8)
     rec["key"][0, : len(key)] = np.frombuffer(key, dtype=np.uint8)
     rec["hp"][0, : len(hp)] = np.frombuffer(hp, dtype=np.uint8)
+    return rec
+
+
+def secret_record(slot: int, suite: int, secret: bytes, *, key_phase: int = 0, v2: bool = False,
+                  updates: int = 0):
+    """One qpp_secret: a connection's traffic secret for KeyTable.derive."""
+    if not 1 <= len(secret) <= 64:
+        raise ValueError("secret must be 1..64 bytes")
+    rec = np.zeros(1, dtype=SECRET)
+    rec["slot"] = slot
+    rec["suite"] = suite
+    rec["key_phase"] = key_phase
+    rec["flags"] = DERIVE_V2 if v2 else 0
+    rec["secret_len"] = len(secret)
+    rec["updates"] = updates
+    rec["secret"][0, : len(secret)] = np.frombuffer(secret, dtype=np.uint8)
     return rec

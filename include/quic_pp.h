@@ -92,6 +92,23 @@ typedef struct qpp_key_material {
     uint8_t hp[32];
 } qpp_key_material;     /* 84 bytes */
 
+/* One connection's traffic secret for the batched key schedule (qpp_keytab_derive). */
+#define QPP_DERIVE_V2 1u    /* QUIC v2 labels "quicv2 key/iv/hp" (quic/crypto.py:52-56) */
+
+typedef struct qpp_secret {
+    uint32_t slot;
+    uint8_t suite;       /* QPP_AES_128_GCM (SHA-256) / QPP_AES_256_GCM (SHA-384) /
+                            QPP_CHACHA20_POLY1305 (SHA-256), tls.py:1108-1112 */
+    uint8_t key_phase;
+    uint8_t flags;       /* QPP_DERIVE_* */
+    uint8_t secret_len;  /* bytes of secret[] used: 1..64 */
+    uint32_t updates;    /* key updates applied first: secret = HKDF-Expand-Label(secret,
+                            "quic ku", "", hash_len) per step (next_key_phase,
+                            quic/crypto.py:157-168; the label is "quic ku" for v2 too) */
+    uint32_t rsv;
+    uint8_t secret[64];
+} qpp_secret;            /* 80 bytes */
+
 typedef struct qpp_keytab qpp_keytab;   /* device-resident expanded keys */
 typedef struct qpp_session qpp_session; /* pinned staging + device buffers + stream */
 
@@ -108,6 +125,13 @@ void qpp_keytab_destroy(qpp_keytab *kt);
 uint32_t qpp_keytab_capacity(const qpp_keytab *kt);
 int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void *stream);
 int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *stream);
+/* Batched CryptoContext.setup (quic/crypto.py:121-136) for n connections at once:
+ * derive_key_iv_hp (quic/crypto.py:34-56 = HKDF-Expand-Label, tls.py:164-185)
+ * on the device, one lane per secret, after `updates` key updates, then the same
+ * slot expansion as qpp_keytab_set.  km_out (host memory, may be NULL) receives
+ * the derived key material, e.g. for the host-side AEAD objects. */
+int qpp_keytab_derive(qpp_keytab *kt, const qpp_secret *sec, uint32_t n,
+                      qpp_key_material *km_out, void *stream);
 
 /* Batched packet protection on device buffers (asynchronous on `stream`).
  * qpp_protect replaces AEAD_encrypt (_crypto.c:157-194) + HeaderProtection_apply

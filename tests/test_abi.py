@@ -66,6 +66,7 @@ def test_record_layouts_match_header():
     assert sizes["qpp_desc"] == L.DESC.itemsize == 40
     assert sizes["qpp_result"] == L.RESULT.itemsize == 16
     assert sizes["qpp_key_material"] == L.KEY_MATERIAL.itemsize == 84
+    assert sizes["qpp_secret"] == L.SECRET.itemsize == 80
     assert L.DESC.fields["pn"][1] == 24 and L.DESC.fields["slot"][1] == 32
     assert L.RESULT.fields["status"][1] == 8
 
