@@ -370,12 +370,14 @@ struct Bufs {
 // 100 MHz s_memrealtime, written by the wave's first active lane.
 #ifdef QPP_PROBE
 constexpr int kProbeSlots = 16;
-__device__ unsigned long long g_probe[8192 * kProbeSlots];
+constexpr uint32_t kProbeWaves = 8192;  // waves recorded (tools/probe.hip caps n)
+__device__ unsigned long long g_probe[kProbeWaves * kProbeSlots];
 #define QPP_PROBE_AT(i)                                                                      \
     do {                                                                                     \
         const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                      \
-        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                              \
-            g_probe[(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * kProbeSlots + (i)] = t_; \
+        const uint32_t w_ = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);             \
+        if (w_ < kProbeWaves && __lane_id() == __ffsll((long long)__ballot(1)) - 1)          \
+            g_probe[w_ * kProbeSlots + (i)] = t_;                                            \
     } while (0)
 #else
 #define QPP_PROBE_AT(i) ((void)0)

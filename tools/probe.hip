@@ -53,6 +53,10 @@ int main(int argc, char **argv)
 {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 65536;
     const int suite = argc > 2 ? atoi(argv[2]) : 0;
+    if (n == 0 || n > kProbeWaves * 16) {  // 16 packets per wave are recorded
+        printf("probe: n must be 1..%u\n", kProbeWaves * 16);
+        return 2;
+    }
     const int hdr = 11, payload = 1173, slot = 1200;
     qpp_keytab *kt = nullptr;
     if (qpp_keytab_create(4, &kt) != QPP_OK) { printf("keytab failed\n"); return 1; }
