@@ -45,6 +45,10 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 #define QPP_BALANCE 1
 #endif
 constexpr bool kBalance = QPP_BALANCE;  // GCM wave balancing (s_setprio)
+#ifndef QPP_BALANCE_ENC
+#define QPP_BALANCE_ENC 1
+#endif
+constexpr bool kBalanceEnc = QPP_BALANCE_ENC;  // ... for protect too
 
 template <int WG>
 struct __attribute__((aligned(16))) GcmSmem {
@@ -844,7 +848,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                             sm.te, B, src, (uint32_t)ioff,
                             (uint32_t)ooff, P.mask, hbits, pre.h0,
                             sm.stage[__builtin_amdgcn_readfirstlane(tid >> 6)][0],
-                            (kBalance && !ENC) ? &sm.progress : nullptr, got_tag);
+                            (kBalance && (!ENC || kBalanceEnc)) ? &sm.progress : nullptr, got_tag);
                         QPP_PROBE_AT(4);
                         P = unpark(scr, gin + bi + ioff, gout + bo + ooff, hlen, clen);
                         gcm_finish<ENC, SUITE>(P, ks, sub, scr, T, tag, got_tag);
