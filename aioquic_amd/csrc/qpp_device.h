@@ -149,25 +149,62 @@ __device__ __forceinline__ uint32_t lane_fresh()
     return l;
 }
 
-// Wave-wide minimum (every lane gets it), by xor-shuffles: lane-serialized
-// LDS atomics on one word cost ~4 cycles per lane, 64 times per wave.
+// A zero vector materialised where it is used (the compiler otherwise keeps
+// one live across the packet loops, and spills it).
+__device__ __forceinline__ u32x4 zero4()
+{
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return u32x4{z, z, z, z};
+}
+
+// Wave-wide minimum, returned wave-uniform.  DPP within each 16-lane row
+// (quad swaps, half-row and row mirrors), then the four row minima by
+// v_readlane: no lane-address registers, which the compiler would otherwise
+// keep live (spilled) across the packet loops for the next reduction.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+constexpr int kDppQuadSwap1 = 0xB1, kDppQuadSwap2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return __builtin_amdgcn_readfirstlane(v);
+    v = min(v, dpp_mov<kDppQuadSwap1>(v));
+    v = min(v, dpp_mov<kDppQuadSwap2>(v));
+    v = min(v, dpp_mov<kDppHalfMirror>(v));
+    v = min(v, dpp_mov<kDppMirror>(v));
+    const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)v, 0),
+                           (uint32_t)__builtin_amdgcn_readlane((int)v, 16));
+    const uint32_t b = min((uint32_t)__builtin_amdgcn_readlane((int)v, 32),
+                           (uint32_t)__builtin_amdgcn_readlane((int)v, 48));
+    return min(a, b);
 }
+
+__device__ __forceinline__ uint64_t min_u64_dpp_step(uint64_t v, uint32_t lo2, uint32_t hi2)
+{
+    const uint64_t w = (uint64_t)hi2 << 32 | lo2;
+    return w < v ? w : v;
+}
+
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
 {
+#define QPP_MIN64_STEP(CTRL)                                                              \
+    v = min_u64_dpp_step(v, dpp_mov<CTRL>((uint32_t)v), dpp_mov<CTRL>((uint32_t)(v >> 32)))
+    QPP_MIN64_STEP(kDppQuadSwap1);
+    QPP_MIN64_STEP(kDppQuadSwap2);
+    QPP_MIN64_STEP(kDppHalfMirror);
+    QPP_MIN64_STEP(kDppMirror);
+#undef QPP_MIN64_STEP
+    uint64_t m = ~0ull;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
-        const uint64_t w = (uint64_t)hi << 32 | lo;
-        v = w < v ? w : v;
+    for (int r = 0; r < 64; r += 16) {
+        const uint64_t w = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), r) << 32 |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, r);
+        m = w < m ? w : m;
     }
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32 |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
+    return m;
 }
 
 // DPP within a quad of lanes (the 4 lanes that share one packet).

@@ -72,7 +72,9 @@ __device__ __forceinline__ void stage_key(GcmSmem<WG> &sm, const KeySlot *slots,
 {
     typedef const __attribute__((address_space(1))) void *gptr_t;
     typedef __attribute__((address_space(3))) void *lptr_t;
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    // wave index as an SGPR and a fresh lane id: this also runs inside the
+    // packet loops, where a kept lane address would be spilled
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = (int)lane_fresh();
     const uint8_t *gt = gtab + (size_t)s * kGhashTabBytes;
     for (int c = w; c < kGhashTabBytes / 1024; c += WG / 64)
         __builtin_amdgcn_global_load_lds((gptr_t)(gt + c * 1024 + l * 16), (lptr_t)(sm.gt + c * 1024),
@@ -394,17 +396,17 @@ __device__ __forceinline__ void park(const Pkt &P, uint8_t *scr)
     *(u32x4 *)(scr + kScrPark) = P.mask;
     *(u32x4 *)(scr + kScrPark + 16) =
         u32x4{(uint32_t)P.pn, (uint32_t)(P.pn >> 32),
-              P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28, 0};
+              P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28,
+              (uint32_t)P.hlen | (uint32_t)P.clen << 16};
 }
-__device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, uint8_t *dst, int hlen,
-                                      int clen)
+__device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, uint8_t *dst)
 {
     Pkt P;
     const u32x4 w = *(const u32x4 *)(scr + kScrPark + 16);
     P.src = src;
     P.dst = dst;
-    P.hlen = hlen;
-    P.clen = clen;
+    P.hlen = (int)(w.w & 0xffff);
+    P.clen = (int)(w.w >> 16);
     P.mask = *(const u32x4 *)(scr + kScrPark);
     P.pn = (uint64_t)w.y << 32 | w.x;
     P.fbm = w.z & 0xff;
@@ -442,7 +444,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                                             const u32x4 hmask, const uint32_t hbits, const u32x4 h0,
                                             uint8_t *stage, uint32_t *progress, u32x4 &got_tag)
 {
-    const LdsTe T{te, (uint32_t)(threadIdx.x & 31) * 4};
+    const LdsTe T{te, (lane_fresh() & 31) * 4};
     const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
     const int n_g = za + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
     const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
@@ -474,7 +476,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     u32x4 acc = (za && sub == pad) ? z : u32x4{0, 0, 0, 0};
     const int q = pad + za;  // sequence position of CT block 0
     // E_K(J0) slot starts at zero: lanes other than the lengths lane add 0
-    *(u32x4 *)(scr + kScrEj0) = u32x4{0, 0, 0, 0};
+    *(u32x4 *)(scr + kScrEj0) = zero4();
     const CtrCache cc = ctr_cache(nonce, rk, T);
     const uint32_t lens_h = bswap((uint32_t)hlen * 8u);
     const uint32_t cin = ioff + (uint32_t)hlen, cout = ooff + (uint32_t)hlen;
@@ -560,10 +562,12 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
     }
-    acc = ghash_mul(acc, lds, (uint32_t)(3 - sub) * 8192u);
+    // lane-derived values recomputed after the loop rather than kept (spilled)
+    const uint32_t lf = lane_fresh();
+    acc = ghash_mul(acc, lds, (uint32_t)(3 - (lf & 3)) * 8192u);
     // the lengths block is the last of the sequence: lane 3, last step
     __builtin_amdgcn_wave_barrier();
-    if (sub == 3) acc ^= *(const u32x4 *)(scr + kScrEj0);
+    if ((lf & 3) == 3) acc ^= *(const u32x4 *)(scr_wave + (lf >> 2) * kScratch + kScrEj0);
     return quad_xor_all(acc);
 }
 
@@ -724,25 +728,39 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
     constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
     constexpr int kPktPerWG = WG / 4;
     __shared__ SuiteSmem<SUITE, WG> sm;
-    const int tid = threadIdx.x, sub = tid & 3, lp = tid >> 2;
-    const uint32_t p = blockIdx.x * kPktPerWG + lp;
-    const bool valid = p < n;
-    uint8_t *scr = sm.scratch[lp];
+    // Thread-derived values are recomputed where they are used, from the
+    // wave index (an SGPR) and a fresh lane id, instead of being kept live
+    // across the packet loops: at 128 VGPRs anything live across the GCM step
+    // loop is spilled to scratch (HBM traffic and latency).
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto tid_now = [&]() -> uint32_t { return (wv << 6) | lane_fresh(); };
+    auto pkt_of = [&](uint32_t t) -> uint32_t { return blockIdx.x * kPktPerWG + (t >> 2); };
     QPP_PROBE_AT(0);
 
     // Prologue: everything that depends only on the descriptor is requested
     // at once (descriptor, then the header bytes that header protection needs),
     // and the key slot is picked with one LDS min-reduction.  Each dependent
     // global access costs microseconds at launch, when every CU issues at once.
-    qpp_desc d = {};
-    if (valid) d = desc[p];
+    uint32_t my_slot0 = kNoSlot;
+    uint64_t in0 = ~0ull, out0 = ~0ull;
+    {
+        const uint32_t p = pkt_of(threadIdx.x);
+        const bool valid = p < n;
+        qpp_desc d = {};
+        if (valid) d = desc[p];
 #ifdef QPP_PROBE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    QPP_PROBE_AT(10);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        QPP_PROBE_AT(10);
 #endif
-    if (tid == 0) {
-        sm.cur_slot[0] = kNoSlot;
-        if constexpr (kGcm) sm.progress = 0;
+        if (threadIdx.x == 0) {
+            sm.cur_slot[0] = kNoSlot;
+            if constexpr (kGcm) sm.progress = 0;
+        }
+        if (valid) {
+            my_slot0 = d.slot;
+            in0 = d.in_off;
+            out0 = d.out_off;
+        }
     }
     // key material: speculate that the workgroup's packets use the slot of
     // its first packet (host batches are grouped by slot) and stage it now
@@ -758,10 +776,6 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
 #ifdef QPP_PROBE
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     QPP_PROBE_AT(11);
-#endif
-    const HdrPre pre = prefetch_hdr<ENC>(d, gin, valid);
-#ifdef QPP_PROBE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     QPP_PROBE_AT(12);
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged key slot (LDS-DMA)
@@ -769,21 +783,21 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
 #ifdef QPP_PROBE
     QPP_PROBE_AT(13);
 #endif
-    const uint32_t my_slot = valid ? d.slot : kNoSlot;
-    bool done = !valid;
     {
-        const uint32_t m = wave_min_u32(my_slot);
+        const uint32_t m = wave_min_u32(my_slot0);
         if (__lane_id() == 0) atomicMin(&sm.cur_slot[0], m);
     }
     // 32-bit buffer views based at this wave's lowest input / output offsets
-    // (a wave's 16 packets must lie within 4 GiB of each other)
-    const uint64_t bi = wave_min_u64(valid ? d.in_off : ~0ull);
-    const uint64_t bo = wave_min_u64(valid ? d.out_off : ~0ull);
+    // (a wave's 16 packets must lie within 4 GiB of each other); wave-uniform
+    const uint64_t bi = wave_min_u64(in0);
+    const uint64_t bo = wave_min_u64(out0);
     __syncthreads();
     QPP_PROBE_AT(7);
 
-    // one iteration per distinct key slot in the workgroup, lowest first;
-    // cur_slot is double-buffered so the next minimum is reduced meanwhile
+    // One iteration per distinct key slot in the workgroup, lowest first;
+    // cur_slot is double-buffered so the next minimum is reduced meanwhile.
+    // Slots are taken in increasing order, so a packet is done once its slot
+    // is <= the current one: no per-lane state crosses iterations.
     for (int it = 0;; ++it) {
         const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur_slot[it & 1]);
         if (cur == kNoSlot) break;
@@ -794,7 +808,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
-        if (tid == 0) sm.cur_slot[(it + 1) & 1] = kNoSlot;
+        if (wv == 0 && lane_fresh() == 0) sm.cur_slot[(it + 1) & 1] = kNoSlot;
         __syncthreads();
         // GCM reads its key material from the staged LDS copy
         const KeySlot *ks;
@@ -803,23 +817,20 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
         const uint32_t suite = cur < cap ? ks->suite : 0xffu;
         const bool mine = suite == SUITE;
         QPP_PROBE_AT(1);
-        const bool in_slot = !done && my_slot == cur;
-        done = done || in_slot;
+        // the descriptor is re-read each iteration (an L2 hit after the prologue)
+        const uint32_t t1 = tid_now(), p1 = pkt_of(t1);
+        const qpp_desc d = p1 < n ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
+        const bool in_slot = d.slot == cur;
         {
-            const uint32_t m = wave_min_u32(done ? kNoSlot : my_slot);
+            const uint32_t m = wave_min_u32(d.slot > cur ? d.slot : kNoSlot);
             if (__lane_id() == 0 && m != kNoSlot) atomicMin(&sm.cur_slot[(it + 1) & 1], m);
         }
-        if (in_slot && suite > QPP_CHACHA20_POLY1305 && sub == 0)
-            res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
+        if (in_slot && suite > QPP_CHACHA20_POLY1305 && (t1 & 3) == 0)
+            res[p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
         if (in_slot && mine) {
+            const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
             if constexpr (kGcm) {
-                // Re-read the descriptor and header words (L2 hits: the
-                // prologue fetched them) so that neither stays live through
-                // the step loop, where 128 VGPRs leave no room for them.
-                asm volatile("" ::: "memory");
-                const qpp_desc d = desc[p];
-                const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
-                const LdsTe T{sm.te, (uint32_t)(tid & 31) * 4};
+                const LdsTe T{sm.te, (t1 & 31) * 4};
                 Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
                 if (P.status == QPP_S_OK) {
                     // plain keys for rounds 0-2 (counter cache) and NR, rotated between
@@ -835,7 +846,7 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                         const Bufs B{
                             __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
                             __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
-                        const uint8_t *src = P.src;
+                        uint8_t *scr = sm.scratch[t1 >> 2];
                         const int hlen = P.hlen, clen = P.clen;
                         const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 |
                                                (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28;
@@ -844,25 +855,30 @@ __global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slot
                         QPP_PROBE_AT(2);
                         u32x4 got_tag;
                         const u32x4 tag = gcm_packet<kNR, ENC>(
-                            P.nonce, hlen, clen, rk, sub, scr, sm.scratch[__builtin_amdgcn_readfirstlane(tid >> 6) * 16], sm.gt,
-                            sm.te, B, src, (uint32_t)ioff,
-                            (uint32_t)ooff, P.mask, hbits, pre.h0,
-                            sm.stage[__builtin_amdgcn_readfirstlane(tid >> 6)][0],
+                            P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], sm.gt,
+                            sm.te, B, P.src, (uint32_t)ioff,
+                            (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0],
                             (kBalance && (!ENC || kBalanceEnc)) ? &sm.progress : nullptr, got_tag);
                         QPP_PROBE_AT(4);
-                        P = unpark(scr, gin + bi + ioff, gout + bo + ooff, hlen, clen);
-                        gcm_finish<ENC, SUITE>(P, ks, sub, scr, T, tag, got_tag);
+                        // everything below is re-derived after the step loop
+                        const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
+                        const qpp_desc d2 = desc[p2];
+                        uint8_t *scr2 = sm.scratch[t2 >> 2];
+                        P = unpark(scr2, gin + d2.in_off, gout + d2.out_off);
+                        const LdsTe T2{sm.te, (t2 & 31) * 4};
+                        gcm_finish<ENC, SUITE>(P, ks, t2 & 3, scr2, T2, tag, got_tag);
                     } else {
                         P.status = QPP_S_LENGTH;  // workgroup spans more than 4 GiB
                     }
                 }
-                write_result<ENC>(res, p, sub, P);
+                const uint32_t t3 = tid_now();
+                write_result<ENC>(res, pkt_of(t3), t3 & 3, P);
                 QPP_PROBE_AT(5);
             } else {
                 const ConstTe T;
                 Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
-                if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, sub, scr);
-                write_result<ENC>(res, p, sub, P);
+                if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, t1 & 3, sm.scratch[t1 >> 2]);
+                write_result<ENC>(res, p1, t1 & 3, P);
             }
         }
         __syncthreads();
