@@ -596,6 +596,30 @@ __device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, u
 
 // ---------------------------------------------------- ChaCha20-Poly1305 --
 
+// Work of a packet's quad (RFC 8439 sec. 2.8; _crypto.c:157-204 / :115-155).
+// Units u = 4k + sub: u < 3 -> ChaCha20 chunk u, u = 3 -> the Poly1305 key
+// block (counter 0, RFC 8439 sec. 2.6), u > 3 -> chunk u - 1.  So lane 3
+// produces the one-time key while lanes 0-2 encrypt chunks 0-2, and a
+// 1173-byte payload (19 chunks + key = 20 units) takes 5 ChaCha blocks per
+// lane instead of 6.  Poly1305 is per-lane Horner over the lane's blocks
+// (r per block; r^8 / r^12 across the 2 / 3 other lanes' chunks) and one
+// quad sum at the end.
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_dpp(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+constexpr int kQuadBcast3 = 0xFF;  // quad_perm [3,3,3,3]
+
+// values the compiler must not keep live across the chunk loop: pass them
+// through an empty asm so powers of r are recomputed after it
+__device__ __forceinline__ P130 launder(P130 x)
+{
+#pragma unroll
+    for (int l = 0; l < 5; ++l) asm volatile("" : "+v"(x.v[l]));
+    return x;
+}
+
 template <bool ENC>
 __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
 {
@@ -608,57 +632,91 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     const uint8_t *pin = P.src + P.hlen;
     uint8_t *pout = P.dst + P.hlen;
 
-    // one-time Poly1305 key = ChaCha20(key, counter 0) (RFC 8439 sec. 2.6)
-    uint32_t blk[16];
-    chacha_block(key, 0, n0, n1, n2, blk);
-    const P130 r = p130_r(blk[0], blk[1], blk[2], blk[3]);
-    const uint32_t s0 = blk[4], s1 = blk[5], s2 = blk[6], s3 = blk[7];
-    const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
-    const P130 r12 = p130_mul(r8, r4);
-
-    P130 acc = p130_zero();
-    int g_last = -1;
-    // lane 0 starts its chain with the associated data (Δ = 1 into chunk 0)
-    if (sub == 0) {
-        for (int g = 0; g < n_a; ++g) {
-            const int nb = min(16, P.hlen - 16 * g);
-            u32x4 x = ld_part(P.src + 16 * g, nb);
-            if (unmask) x ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
-            if (!ENC || !P.hp) st_part(P.dst + 16 * g, x, nb);
-            acc = p130_mul(p130_add(acc, p130_block(x)), r);
-            g_last = g;
-        }
-    }
-    // the 64 input bytes of chunk c, fetched one chunk ahead of use
+    // the 64 input bytes of chunk c
     auto fetch = [&](int c, u32x4 (&v)[4]) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int i = 4 * c + t;
-            v[t] = i < n_c ? ld_part(pin + 16 * i, min(16, P.clen - 16 * i)) : u32x4{0, 0, 0, 0};
+            v[t] = (c >= 0 && i < n_c) ? ld_part(pin + 16 * i, min(16, P.clen - 16 * i))
+                                       : u32x4{0, 0, 0, 0};
         }
     };
-    u32x4 nxt[4];
-    if (sub < chunks) fetch(sub, nxt);
-    // acc already carries one factor r per folded block: h = (h + m) * r
-    for (int c = sub; c < chunks; c += 4) {
-        u32x4 cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
-        if (c + 4 < chunks) fetch(c + 4, nxt);
-        chacha_block(key, (uint32_t)(1 + c), n0, n1, n2, blk);
-        // jump from this lane's previous block to the first block of chunk c
-        if (g_last >= 0 && c >= 4) acc = p130_mul(acc, r12);  // gap of 13 blocks: r^12, then r^1 per block
+    // keystream chunk c: xor, store, and the Poly1305 input blocks (ciphertext)
+    auto crypt = [&](int c, const u32x4 (&din)[4], const uint32_t (&blk)[16], u32x4 (&x)[4]) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int i = 4 * c + t;
-            if (i >= n_c) break;
+            x[t] = u32x4{0, 0, 0, 0};
+            if (i >= n_c) continue;
             const int nb = min(16, P.clen - 16 * i);
-            const u32x4 din = cur[t];
-            const u32x4 ksb = u32x4{blk[4 * t], blk[4 * t + 1], blk[4 * t + 2], blk[4 * t + 3]};
-            const u32x4 dout = din ^ ksb;
+            const u32x4 dout = din[t] ^ u32x4{blk[4 * t], blk[4 * t + 1], blk[4 * t + 2], blk[4 * t + 3]};
             st_part(pout + 16 * i, dout, nb);
-            const u32x4 x = keep_bytes(ENC ? dout : din, nb);
-            if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x;
-            acc = p130_mul(p130_add(acc, p130_block(x)), r);
-            g_last = n_a + i;
+            x[t] = keep_bytes(ENC ? dout : din[t], nb);
+            if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[t];
+        }
+    };
+
+    // ---- unit 0..3: chunks 0-2 on lanes 0-2, the one-time key on lane 3
+    const int c0 = sub < 3 ? sub : -1;
+    u32x4 cur[4], x[4];
+    fetch(c0 < chunks ? c0 : -1, cur);
+    uint32_t blk[16];
+    chacha_block(key, sub == 3 ? 0u : (uint32_t)(1 + sub), n0, n1, n2, blk);
+    uint32_t kw[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) kw[w] = quad_dpp<kQuadBcast3>(blk[w]);
+    // s waits in LDS until the tag (scratch [64, 80): unused by this suite)
+    *(u32x4 *)(scr + 64) = u32x4{kw[4], kw[5], kw[6], kw[7]};
+    const P130 r = p130_r(kw[0], kw[1], kw[2], kw[3]);
+    if (c0 >= 0 && c0 < chunks) crypt(c0, cur, blk, x);
+
+    // next unit's input, fetched one unit ahead
+    u32x4 nxt[4];
+    fetch(3 + sub < chunks ? 3 + sub : -1, nxt);
+
+    P130 acc = p130_zero();
+    int g_last = -1;
+    // lane 0 starts its chain with the associated data
+    if (sub == 0) {
+        for (int g = 0; g < n_a; ++g) {
+            const int nb = min(16, P.hlen - 16 * g);
+            u32x4 a = ld_part(P.src + 16 * g, nb);
+            if (unmask) a ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
+            if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
+            acc = p130_mul(p130_add(acc, p130_block(a)), r);
+            g_last = g;
+        }
+    }
+    if (c0 >= 0 && c0 < chunks) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (4 * c0 + t >= n_c) break;
+            acc = p130_mul(p130_add(acc, p130_block(x[t])), r);
+            g_last = n_a + 4 * c0 + t;
+        }
+    }
+    P130 r12;
+    {
+        const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
+        r12 = p130_mul(r8, r4);
+        // the first jump of lanes 0-2 skips the 2 chunks between theirs (r^8)
+        if (sub < 3 && g_last >= 0 && 3 + sub < chunks) acc = p130_mul(acc, r8);
+    }
+    // ---- units 4k + sub, k >= 1: chunk 4k + sub - 1; later jumps skip 3 chunks (r^12)
+    bool first = true;
+    for (int c = 3 + sub; c < chunks; c += 4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cur[t] = nxt[t];
+        fetch(c + 4 < chunks ? c + 4 : -1, nxt);
+        chacha_block(key, (uint32_t)(1 + c), n0, n1, n2, blk);
+        crypt(c, cur, blk, x);
+        if (!first && g_last >= 0) acc = p130_mul(acc, r12);
+        first = false;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (4 * c + t >= n_c) break;
+            acc = p130_mul(p130_add(acc, p130_block(x[t])), r);
+            g_last = n_a + 4 * c + t;
         }
     }
     // acc = sum m_g r^(g_last - g + 1); scale to r^(n_g - g) with r^(n_g - 1 - g_last)
@@ -666,14 +724,16 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     if (g_last < 0) e = 0;
     P130 f = acc;
     if (e > 1) {
-        // square-and-multiply over r^1, r^2, r^4, r^8, r^16 (e <= 17)
+        // square-and-multiply over r^1, r^2, r^4, r^8, r^16 (e <= 17), powers
+        // recomputed here rather than kept through the loop
+        const P130 rr = launder(r);
+        const P130 r2 = p130_mul(rr, rr), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
         const int m = e - 1;
-        const P130 r16 = p130_mul(r8, r8);
-        if (m & 1) f = p130_mul(f, r);
+        if (m & 1) f = p130_mul(f, rr);
         if (m & 2) f = p130_mul(f, r2);
         if (m & 4) f = p130_mul(f, r4);
         if (m & 8) f = p130_mul(f, r8);
-        if (m & 16) f = p130_mul(f, r16);
+        if (m & 16) f = p130_mul(f, p130_mul(r8, r8));
     }
     // sum over the quad (limbs < 2^28 each, no carries needed), add the lengths block
     P130 sum;
@@ -686,7 +746,8 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     }
     const u32x4 lens = u32x4{(uint32_t)P.hlen, 0u, (uint32_t)P.clen, 0u};
     sum = p130_mul(p130_add(sum, p130_block(lens)), r);
-    const u32x4 tag = p130_finish(sum, s0, s1, s2, s3);
+    const u32x4 sw = *(const u32x4 *)(scr + 64);
+    const u32x4 tag = p130_finish(sum, sw.x, sw.y, sw.z, sw.w);
     if (ENC) {
         if (sub == 0) st16(pout + P.clen, tag);
         if (P.hp) protect_finish_hp<QPP_CHACHA20_POLY1305>(P, ks, sub, scr, tag, ConstTe{});
