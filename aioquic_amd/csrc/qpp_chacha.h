@@ -37,6 +37,40 @@ __device__ __forceinline__ void chacha_block(const uint32_t *key, uint32_t ctr, 
     out[8] = x8 + key[4]; out[9] = x9 + key[5]; out[10] = x10 + key[6]; out[11] = x11 + key[7];
     out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
 }
+
+// One ChaCha20 block computed by the 4 lanes of a quad together (all four
+// hold the same inputs): lane j keeps column j (words j, 4+j, 8+j, 12+j), the
+// column rounds are lane-local and the diagonal rounds rotate rows 1-3 by
+// 1/2/3 lanes with DPP.  ~30 VALU per double round and 4 state registers, for
+// the header-protection block every lane of the quad needs (sec. 5.4.4 of
+// RFC 9001), instead of 96 VALU and 16 registers per lane for a private copy.
+// Returns output words 0..3 (the first 16 keystream bytes) in every lane.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ u32x4 chacha_block_quad_row0(const uint32_t *key, uint32_t ctr,
+                                                        uint32_t n0, uint32_t n1, uint32_t n2,
+                                                        int sub)
+{
+    constexpr int kRot1 = 0x39, kRot2 = 0x4E, kRot3 = 0x93;  // lane j <- lane j+1 / j+2 / j+3
+    const uint32_t sig = sub == 0 ? 0x61707865u : sub == 1 ? 0x3320646eu : sub == 2 ? 0x79622d32u : 0x6b206574u;
+    const uint32_t kb = sub == 0 ? key[0] : sub == 1 ? key[1] : sub == 2 ? key[2] : key[3];
+    const uint32_t kc = sub == 0 ? key[4] : sub == 1 ? key[5] : sub == 2 ? key[6] : key[7];
+    const uint32_t kd = sub == 0 ? ctr : sub == 1 ? n0 : sub == 2 ? n1 : n2;
+    uint32_t a = sig, b = kb, c = kc, d = kd;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        QPP_QR(a, b, c, d);
+        b = qdpp<kRot1>(b); c = qdpp<kRot2>(c); d = qdpp<kRot3>(d);
+        QPP_QR(a, b, c, d);
+        b = qdpp<kRot3>(b); c = qdpp<kRot2>(c); d = qdpp<kRot1>(d);
+    }
+    a += sig;  // output word `sub` of row 0
+    return u32x4{qdpp<0x00>(a), qdpp<0x55>(a), qdpp<0xAA>(a), qdpp<0xFF>(a)};
+}
 #undef QPP_QR
 
 // ------------------------------------------------------------ Poly1305 ----

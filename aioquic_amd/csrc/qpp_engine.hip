@@ -152,6 +152,17 @@ __device__ __forceinline__ u32x4 lds_sample(const uint8_t *scr, int s)
 
 // HeaderProtection_mask (_crypto.c:278-287): AES-ECB(hp, sample), or the
 // first ChaCha20 block with counter = sample[0:4] and nonce = sample[4:16].
+// The same, computed jointly by a packet's quad (every lane holds the same
+// sample): ChaCha20 by columns across the quad; AES as above.
+template <int SUITE, class TE>
+__device__ __forceinline__ u32x4 hp_mask_quad(const KeySlot *ks, u32x4 sample, const TE &T, int sub)
+{
+    if constexpr (SUITE == QPP_CHACHA20_POLY1305)
+        return chacha_block_quad_row0(ks->hrk, sample.x, sample.y, sample.z, sample.w, sub);
+    else
+        return aes_encrypt<SUITE == QPP_AES_256_GCM ? 14 : 10>(sample, ks->hrk, T);
+}
+
 template <int SUITE, class TE>
 __device__ __forceinline__ u32x4 hp_mask_of(const KeySlot *ks, u32x4 sample, const TE &T)
 {
@@ -264,7 +275,7 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const HdrPre &pre, c
         if (P.pn_off < 1 || P.pn_off + 20 > len || P.pn_off > QPP_MAX_HDR - 4) {
             P.status = QPP_S_LENGTH;
         } else {
-            P.mask = hp_mask_of<SUITE>(ks, pre.smp, T);
+            P.mask = hp_mask_quad<SUITE>(ks, pre.smp, T, (int)(lane_fresh() & 3));
             uint32_t b0 = pre.b0;
             P.fbm = first_byte_mask(b0);
             b0 ^= byte_of(P.mask, 0) & P.fbm;
@@ -306,7 +317,7 @@ __device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int
     }
     __builtin_amdgcn_wave_barrier();
     const u32x4 sample = lds_sample(scr, 4 - P.pn_len);
-    P.mask = hp_mask_of<SUITE>(ks, sample, T);
+    P.mask = hp_mask_quad<SUITE>(ks, sample, T, sub);
     const int n_a = (P.hlen + 15) >> 4;
     for (int q = sub; q < n_a; q += 4) {
         const int nb = min(16, P.hlen - 16 * q);
@@ -1289,16 +1300,18 @@ int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *st
 // Workgroup size per suite family (tuned on MI355X; overridable for sweeps
 // with QPP_WG_GCM / QPP_WG_CHACHA = 512 | 768 | 1024).
 static const int kGcmWG = 1024;
-static const int kChachaWG = 512;
+static const int kChachaWGEnc = 256, kChachaWGDec = 256;  // measured: tools/sweep_wg.sh
 
-static int wg_choice(const char *env, int dflt)
+// workgroup size overrides for experiments (QPP_WG_GCM, QPP_WG_CHACHA_ENC /
+// _DEC); only the sizes instantiated below are accepted
+static int wg_choice(const char *env, int dflt, bool chacha)
 {
     const char *v = getenv(env);
     if (!v) return dflt;
     const int w = atoi(v);
+    if (chacha) return (w == 256 || w == 512 || w == 1024) ? w : dflt;
     return (w == 512 || w == 768 || w == 1024) ? w : dflt;
 }
-
 
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                           const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream)
@@ -1309,7 +1322,9 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     // one launch per suite installed in the table (an empty table still
     // gets one launch so every packet reports QPP_S_NO_KEY)
     const uint32_t mask = kt->suite_mask ? kt->suite_mask : 1u;
-    const int wg_gcm = wg_choice("QPP_WG_GCM", kGcmWG), wg_cc = wg_choice("QPP_WG_CHACHA", kChachaWG);
+    const int wg_gcm = wg_choice("QPP_WG_GCM", kGcmWG, false);
+    const int wg_cc = enc ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
+                          : wg_choice("QPP_WG_CHACHA_DEC", kChachaWGDec, true);
 #define QPP_LAUNCH_WG(SUITE, WGV)                                                              \
     do {                                                                                       \
         const dim3 grid((n + WGV / 4 - 1) / (WGV / 4)), block(WGV);                            \
@@ -1320,17 +1335,22 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
             hipLaunchKernelGGL((k_packets<SUITE, false, WGV>), grid, block, 0, s, kt->d_slots, \
                                kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);            \
     } while (0)
-#define QPP_LAUNCH(SUITE, WGSEL)                                                               \
+#define QPP_LAUNCH_GCM(SUITE)                                                                  \
     if (mask & (1u << SUITE)) {                                                                \
-        if (WGSEL == 512) QPP_LAUNCH_WG(SUITE, 512);                                           \
-        else if (WGSEL == 768) QPP_LAUNCH_WG(SUITE, 768);                                      \
+        if (wg_gcm == 512) QPP_LAUNCH_WG(SUITE, 512);                                          \
+        else if (wg_gcm == 768) QPP_LAUNCH_WG(SUITE, 768);                                     \
         else QPP_LAUNCH_WG(SUITE, 1024);                                                       \
         HIPCHK(hipGetLastError());                                                             \
     }
-    QPP_LAUNCH(QPP_AES_128_GCM, wg_gcm)
-    QPP_LAUNCH(QPP_AES_256_GCM, wg_gcm)
-    QPP_LAUNCH(QPP_CHACHA20_POLY1305, wg_cc)
-#undef QPP_LAUNCH
+    QPP_LAUNCH_GCM(QPP_AES_128_GCM)
+    QPP_LAUNCH_GCM(QPP_AES_256_GCM)
+    if (mask & (1u << QPP_CHACHA20_POLY1305)) {
+        if (wg_cc == 256) QPP_LAUNCH_WG(QPP_CHACHA20_POLY1305, 256);
+        else if (wg_cc == 1024) QPP_LAUNCH_WG(QPP_CHACHA20_POLY1305, 1024);
+        else QPP_LAUNCH_WG(QPP_CHACHA20_POLY1305, 512);
+        HIPCHK(hipGetLastError());
+    }
+#undef QPP_LAUNCH_GCM
 #undef QPP_LAUNCH_WG
     return QPP_OK;
 }

@@ -1,12 +1,14 @@
 #!/bin/bash
-# Workgroup-size sweep of the packet kernels (GPU box).  Prints one JSON line per variant.
+# Workgroup-size sweep of the packet kernels (GPU box).  One line per variant.
+#   CFG=3 tools/sweep_wg.sh   (ChaCha: QPP_WG_CHACHA_ENC/DEC in 256 512 1024)
+#   CFG=2 tools/sweep_wg.sh   (GCM: QPP_WG_GCM in 512 768 1024)
 set -uo pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-for cfg in ${CONFIGS:-2 3}; do
-  for wg in 512 768 1024; do
-    if [ "$cfg" = "3" ]; then export QPP_WG_CHACHA=$wg; unset QPP_WG_GCM; else export QPP_WG_GCM=$wg; unset QPP_WG_CHACHA; fi
-    timeout -k 10 120 python bench.py --config $cfg --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/sweep_${cfg}_${wg}.json 2>/dev/null || { echo "fail cfg=$cfg wg=$wg"; exit 1; }
-    python -c "import json,sys; d=json.load(open('gpurun_out/sweep_${cfg}_${wg}.json')); print('cfg', $cfg, 'wg', $wg, d['value'], d['kernels_ms'], d['status_ok'])"
-  done
+CFG=${CFG:-3}
+if [ "$CFG" = 3 ]; then SIZES="256 512 1024"; VARS="QPP_WG_CHACHA_ENC QPP_WG_CHACHA_DEC"; else SIZES="512 768 1024"; VARS="QPP_WG_GCM"; fi
+for wg in $SIZES; do
+  for v in $VARS; do export $v=$wg; done
+  timeout -k 10 120 python bench.py --config $CFG --steps 30 --warmup 3 --cpu-seconds 0 > gpurun_out/sweep_${CFG}_${wg}.json 2>/dev/null || { echo "fail cfg=$CFG wg=$wg"; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/sweep_${CFG}_${wg}.json')); print('cfg', $CFG, 'wg', $wg, d['value'], d['kernels_ms'], d['status_ok'])"
 done
