@@ -166,6 +166,39 @@ def cpu_baseline(w, seconds: float, cfg, procs: int = 1):
 # --------------------------------------------------------------------- main --
 
 
+def hbm_copy_gbs(dev, nbytes=1 << 30, reps=10):
+    """Attainable HBM bandwidth on this box: a device-to-device copy of 1 GiB
+    (read + write bytes / time), the practical ceiling beside the 8 TB/s spec."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / reps
+    del a, b
+    return round(2 * nbytes / t / 1e9, 1)
+
+
+def measured_traffic(workload, n, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    passes (profiles/traffic.json, tools/traffic.py), when they were taken on
+    this workload at this packet count."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        entry = json.load(open(path))[workload]
+    except (OSError, KeyError, ValueError):
+        return {}
+    if entry.get("packets") != n or kernel not in entry:
+        return {}
+    return {"bytes": entry[kernel]["bytes"], "source": entry["source"]}
+
+
 def key_schedule(eng_cls, n_keys, suite, version):
     """Batched CryptoContext.setup for n_keys connections: the device path
     (qpp_keytab_derive: HKDF + slot expansion, synchronous) against the host
@@ -278,9 +311,11 @@ def main():
 
     total_bytes = float(n) * 1200 * args.steps * world
     value = total_bytes / elapsed / GIB
+    copy_gbs = hbm_copy_gbs(dev) if rank == 0 else None
     kern_t = max(t_prot, t_unp)
     dom = "protect" if t_prot >= t_unp else "unprotect"
     achieved = BYTES_PER_PKT_KERNEL * n / kern_t / 1e9
+    traffic = measured_traffic(cfg["name"], n, dom)
 
     out = None
     if rank == 0:
@@ -303,7 +338,12 @@ def main():
             "kernel_gib_s": round(n * 1200 / (t_prot + t_unp) / GIB, 3),
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic.get("bytes"),
+                         "traffic_source": traffic.get("source"),
+                         "algorithmic_bytes": BYTES_PER_PKT_KERNEL * n,
+                         "attainable_copy": copy_gbs,
+                         "frac_of_attainable": round(achieved / copy_gbs, 4) if copy_gbs else None},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "status_ok": ok,

@@ -42,6 +42,7 @@ def main():
             rb, wb = fetch[k] * FETCH_CORR, write[k] * WRITE_CORR
             entry[k] = {"read_bytes": round(rb), "write_bytes": round(wb), "bytes": round(rb + wb),
                         "fetch_size_kib_raw": round(fetch[k] / 1024), "write_size_kib_raw": round(write[k] / 1024)}
+    entry["packets"] = int(sys.argv[sys.argv.index("--packets") + 1]) if "--packets" in sys.argv else 65536
     entry["source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes ({fdir}, {wdir}); "
                        f"corrections x{FETCH_CORR:.3f} / x{WRITE_CORR:.3f} from tools/calib_hbm.hip")
     data[name] = entry
