@@ -388,6 +388,70 @@ __device__ __forceinline__ u32x4 aes_ctr(const CtrCache &c, uint32_t cb, const u
 
 // --------------------------------------------------------------- GHASH ----
 
+// One window pair of a GHASH product (see ghash_mul): windows 2j (low nibble)
+// and 2j+1 (high nibble) of byte j of y, tables of one power at LDS `tab`.
+__device__ __forceinline__ u32x4 ghash_pair(const uint32_t (&yw)[4], int j, const uint8_t *lds,
+                                            uint32_t tab, u32x4 acc)
+{
+    const int d = j >> 2;
+    const uint32_t sel = 0x0c0c0c00u | (uint32_t)(j & 3);
+    const uint32_t alo = __builtin_amdgcn_perm(0u, (yw[d] << 4) & 0xF0F0F0F0u, sel);
+    const uint32_t ahi = __builtin_amdgcn_perm(0u, yw[d] & 0xF0F0F0F0u, sel);
+    const u32x4 e0 = *(const u32x4 *)(lds + tab + (2 * j) * 256 + alo);
+    const u32x4 e1 = *(const u32x4 *)(lds + tab + (2 * j + 1) * 256 + ahi);
+    return xor3(acc, e0, e1);
+}
+
+// AES-CTR block (as aes_ctr) with the product g = y * H^p woven into its LDS
+// phases: the AES rounds are a chain of dependent table reads, so each phase
+// also issues QPP_GH_PER_PHASE independent GHASH window pairs, and the 16
+// pairs of the product ride on the AES phases' LDS latency instead of forming
+// phases of their own.  sched_barrier fences each phase so that the compiler
+// neither hoists all 32 GHASH reads (128 VGPRs) nor regroups them.
+#ifndef QPP_GH_PER_PHASE
+#define QPP_GH_PER_PHASE 2
+#endif
+template <int NR, class TE>
+__device__ __forceinline__ u32x4 aes_ctr_gh(const CtrCache &c, uint32_t cb, const uint32_t *rk,
+                                            const TE &T, const u32x4 y, const uint8_t *lds,
+                                            uint32_t tab, u32x4 &g)
+{
+    constexpr int kPer = QPP_GH_PER_PHASE;
+    const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+    u32x4 ga = {0, 0, 0, 0};
+    // the window pairs of LDS phase p (0: u0, 1: round 2's words, r - 1: round r)
+    auto gh = [&](int p) {
+#pragma unroll
+        for (int e = 0; e < kPer; ++e)
+            if (p * kPer + e < 16) ga = ghash_pair(yw, p * kPer + e, lds, tab, ga);
+    };
+    const uint32_t u0 = c.c0 ^ T.t3(rk[3] ^ (cb << 24));
+    gh(0);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t s0 = c.d0 ^ T.t0(u0), s1 = c.d1 ^ T.t3(u0), s2 = c.d2 ^ T.t2(u0), s3 = c.d3 ^ T.t1(u0);
+    gh(1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 3; r < NR; ++r) {
+        const uint32_t *k = rk + 4 * r;
+        const uint32_t t0 = xor3(T.t0(s0), T.t1(s1), rotl(xor3(T.t2r(s2), T.t3r(s3), k[0]), 16));
+        const uint32_t t1 = xor3(T.t0(s1), T.t1(s2), rotl(xor3(T.t2r(s3), T.t3r(s0), k[1]), 16));
+        const uint32_t t2 = xor3(T.t0(s2), T.t1(s3), rotl(xor3(T.t2r(s0), T.t3r(s1), k[2]), 16));
+        const uint32_t t3 = xor3(T.t0(s3), T.t1(s0), rotl(xor3(T.t2r(s1), T.t3r(s2), k[3]), 16));
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        gh(r - 1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = kPer * (NR - 1); j < 16; ++j) ga = ghash_pair(yw, j, lds, tab, ga);
+    g = ga;
+    const uint32_t *k = rk + 4 * NR;
+    return u32x4{(T.f0(s0) | T.f1(s1) | T.f2(s2) | T.f3(s3)) ^ k[0],
+                 (T.f0(s1) | T.f1(s2) | T.f2(s3) | T.f3(s0)) ^ k[1],
+                 (T.f0(s2) | T.f1(s3) | T.f2(s0) | T.f3(s1)) ^ k[2],
+                 (T.f0(s3) | T.f1(s0) | T.f2(s1) | T.f3(s2)) ^ k[3]};
+}
+
 // x * H^p using the 32 windowed tables of power p at LDS byte offset `tab`.
 // Entry address = tab + w*256 + v*16: the w*256 part folds into the ds_read
 // immediate; (word & 0xF0F0F0F0) already holds high-nibble*16 per byte.

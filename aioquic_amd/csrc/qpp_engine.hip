@@ -49,6 +49,15 @@ constexpr bool kBalance = QPP_BALANCE;  // GCM wave balancing (s_setprio)
 #define QPP_BALANCE_ENC 1
 #endif
 constexpr bool kBalanceEnc = QPP_BALANCE_ENC;  // ... for protect too
+#ifndef QPP_FUSE_GH
+#define QPP_FUSE_GH 0  // GCM: weave a step's H^4 product into the next block's AES (measured slower)
+#endif
+#ifndef QPP_VMCNT1
+#define QPP_VMCNT1 0  // GCM step loop: wait for the LDS-DMA only, not the last store (no gain)
+#endif
+#ifndef QPP_CHACHA_WPE
+#define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget)
+#endif
 
 template <int WG>
 struct __attribute__((aligned(16))) GcmSmem {
@@ -495,10 +504,20 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     // one block of the sequence: CT block i (input `raw` loaded from CT offset
     // min(16 i, clen - 16) for protect, i.e. end-aligned for a partial tail),
     // the lengths block (i == n_c), or padding
-    auto step = [&](int i, bool last, u32x4 raw) {
+    auto step = [&](int i, bool last, bool first, u32x4 raw) {
         const bool is_ct = i >= 0 && 16 * i < clen;
         const LdsTe Tl{te, (lane_fresh() & 31) * 4};
+#if QPP_FUSE_GH
+        // the previous steps' H^4 product rides on this block's AES phases
+        // (the first step's product is discarded: acc holds Z or 0 there)
+        u32x4 gm;
+        const u32x4 ksb =
+            aes_ctr_gh<NR>(cc, is_ct ? (uint32_t)(i + 2) : 1u, rk, Tl, acc, lds, kTabH4, gm);
+        if (!first) acc = gm;
+#else
+        (void)first;
         const u32x4 ksb = aes_ctr<NR>(cc, is_ct ? (uint32_t)(i + 2) : 1u, rk, Tl);
+#endif
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
         uint32_t soff = kOob;
         if (is_ct) {
@@ -517,12 +536,14 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         }
         __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, 0);
         acc ^= x;
-        // AES and GHASH of a step are independent for unprotect; overlapping
-        // them would need more than the 128 VGPRs of 4 waves/SIMD
+#if !QPP_FUSE_GH
         __builtin_amdgcn_sched_barrier(0);
         // H^4 inside the loop (table offset folds into the ds_read immediates);
         // the last step's H^(4-j) is applied after the loop
         if (!last) acc = ghash_mul(acc, lds, kTabH4);
+#else
+        (void)last;
+#endif
     };
     // buffer offset of CT block i's input (or out of range)
     auto ct_load = [&](int i) -> uint32_t {
@@ -536,7 +557,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         QPP_PROBE_AT(3);
         // the staged bytes as an end-aligned load would see them
         const u32x4 st = *(const u32x4 *)(scr + kScrTail);
-        step(sub - q, true, shl_bytes(st, 16 - rlen));
+        step(sub - q, true, true, shl_bytes(st, 16 - rlen));
     } else {
         // LDS-DMA staging: lane l's 16 bytes land at stage[buf][16 l]
         auto dma = [&](uint32_t off, int buf) {
@@ -562,12 +583,20 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                 else __builtin_amdgcn_s_setprio(0);
                 ++it;
             }
-            // the compiler does not track LDS-DMA: retire it explicitly
+            // the compiler does not track LDS-DMA: retire it explicitly.  After
+            // the first step the one vector-memory op issued after this DMA is
+            // the previous step's store; gfx950 retires them in issue order,
+            // so vmcnt(1) waits for the DMA but not for that write-back
+#if QPP_VMCNT1
+            if (k == S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+#else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             const u32x4 raw = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
             // next step's block; on the last step the received tag
             dma((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4), b ^ 1);
-            step(i, k == 1, raw);
+            step(i, k == 1, k == S, raw);
         }
         __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -790,7 +819,7 @@ using SuiteSmem =
 
 
 template <int SUITE, bool ENC, int WG>
-__global__ __launch_bounds__(WG) void k_packets(const KeySlot *__restrict__ slots,
+__global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WPE : 1)) void k_packets(const KeySlot *__restrict__ slots,
                                                 const uint8_t *__restrict__ gtab, uint32_t cap,
                                                 const qpp_desc *__restrict__ desc, uint32_t n,
                                                 const uint8_t *gin, uint8_t *gout,

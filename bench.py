@@ -28,6 +28,12 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_PKT_KERNEL = 1184 + 1200 + 40 + 16  # algorithmic HBM bytes per packet per kernel
+# The GCM kernels' binding resource is the LDS array, not HBM:
+# LDS-array cycles per 1200 B packet per kernel from the instruction mix
+# (ds_read_b32 = 2 cycles, ds_read_b128 = 4 cycles per wave instruction,
+# MI355X_MICROARCH.md sec. LDS), at 256 CUs and 2.4 GHz.
+LDS_CYCLES_PER_PKT = {0: 506.0, 1: 666.0}  # AES-128-GCM, AES-256-GCM
+N_CU, CLOCK_GHZ = 256, 2.4
 
 CONFIGS = {
     2: dict(name="aes-128-gcm 64Ki x 1200B, 1 key", n=65536, suite=0, n_keys=1, version=1),
@@ -52,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-all-cores", type=int, default=1,
                     help="also time the reference on every host core of this GPU's share")
     ap.add_argument("--e2e", action="store_true", help="also time pinned H2D->kernels->D2H")
+    ap.add_argument("--e2e-packets", type=int, default=1 << 20,
+                    help="packets of the end-to-end run (the north star's 1Mi)")
     ap.add_argument("--e2e-chunks", type=int, default=16)
     ap.add_argument("--e2e-streams", type=int, default=4)
     ap.add_argument("--check", action="store_true", help="verify round trip after timing")
@@ -316,6 +324,13 @@ def main():
     dom = "protect" if t_prot >= t_unp else "unprotect"
     achieved = BYTES_PER_PKT_KERNEL * n / kern_t / 1e9
     traffic = measured_traffic(cfg["name"], n, dom)
+    floor = None
+    if not cfg.get("mixed") and cfg["suite"] in LDS_CYCLES_PER_PKT:
+        cyc = LDS_CYCLES_PER_PKT[cfg["suite"]]
+        floor_us = cyc * n / N_CU / (CLOCK_GHZ * 1e3)
+        floor = {"resource": "LDS array", "cycles_per_packet": cyc, "clock_ghz": CLOCK_GHZ,
+                 "floor_us": round(floor_us, 2), "kernel_us": round(kern_t * 1e6, 2),
+                 "frac": round(floor_us / (kern_t * 1e6), 4)}
 
     out = None
     if rank == 0:
@@ -343,7 +358,8 @@ def main():
                          "traffic_source": traffic.get("source"),
                          "algorithmic_bytes": BYTES_PER_PKT_KERNEL * n,
                          "attainable_copy": copy_gbs,
-                         "frac_of_attainable": round(achieved / copy_gbs, 4) if copy_gbs else None},
+                         "frac_of_attainable": round(achieved / copy_gbs, 4) if copy_gbs else None,
+                         "compute_floor": floor},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "status_ok": ok,
@@ -351,18 +367,26 @@ def main():
         if w.n_keys >= 64:
             out["key_schedule"] = key_schedule(PacketEngine, w.n_keys, cfg["suite"], cfg["version"])
         if args.e2e:
-            out["e2e"] = e2e(eng, w, dev, n, chunks=args.e2e_chunks, n_streams=args.e2e_streams)
+            out["e2e"] = e2e(PacketEngine, cfg, 0x9001 + args.config, dev, args.e2e_packets,
+                             chunks=args.e2e_chunks, n_streams=args.e2e_streams)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def e2e(eng, w, dev, n, chunks=16, n_streams=4, reps=5):
+def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5):
     """Pinned host -> H2D -> protect -> unprotect -> D2H, pipelined over
     `n_streams` streams in `chunks` slices (the path starts and ends in UDP
-    socket buffers)."""
+    socket buffers), on its own workload of `n` packets (the north star's
+    1Mi x 1200 B by default).  Verifies the round trip."""
     import torch
+    from aioquic_amd.bench_data import make_workload
+
+    w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=seed,
+                      version=cfg["version"], mixed=cfg.get("mixed"))
+    eng = eng_cls(w.n_keys)
+    eng.set_key_records(w.keys)
 
     h_in = torch.from_numpy(w.plain).pin_memory()
     h_out = torch.empty_like(h_in).pin_memory()
@@ -413,7 +437,9 @@ def e2e(eng, w, dev, n, chunks=16, n_streams=4, reps=5):
             h_out.copy_(d_out, non_blocking=True)
     torch.cuda.synchronize(dev)
     leg["duplex"] = round(reps * h_in.numel() / (time.perf_counter() - t0) / GIB, 3)
-    return {"gib_s": round(per * chunks * 1200 / t / GIB, 3), "chunks": chunks,
+    ok = bool(np.array_equal(h_out.numpy()[: per * chunks * 1200], w.plain[: per * chunks * 1200]))
+    return {"gib_s": round(per * chunks * 1200 / t / GIB, 3), "packets": per * chunks,
+            "round_trip_ok": ok, "chunks": chunks,
             "streams": n_streams, "h2d_gib_s": leg["h2d"], "d2h_gib_s": leg["d2h"],
             "duplex_gib_s_each_way": leg["duplex"],
             "note": f"pinned H2D + protect + unprotect + D2H, {n_streams} streams"}

@@ -53,10 +53,14 @@ int main(int argc, char **argv)
 {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 65536;
     const int suite = argc > 2 ? atoi(argv[2]) : 0;
+#ifdef QPP_PROBE
     if (n == 0 || n > kProbeWaves * 16) {  // 16 packets per wave are recorded
         printf("probe: n must be 1..%u\n", kProbeWaves * 16);
         return 2;
     }
+#else
+    if (n == 0) return 2;
+#endif
     const int hdr = 11, payload = 1173, slot = 1200;
     qpp_keytab *kt = nullptr;
     if (qpp_keytab_create(4, &kt) != QPP_OK) { printf("keytab failed\n"); return 1; }
@@ -117,8 +121,8 @@ int main(int argc, char **argv)
                (double)n * 1200 / ((tp + tu) * 1e-3) / (1u << 30));
         return 0;
     }
-    const int wg = suite == QPP_CHACHA20_POLY1305 ? wg_choice("QPP_WG_CHACHA", kChachaWG)
-                                                  : wg_choice("QPP_WG_GCM", kGcmWG);
+    const int wg = suite == QPP_CHACHA20_POLY1305 ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
+                                                  : wg_choice("QPP_WG_GCM", kGcmWG, false);
     const int waves = (int)(((n + wg / 4 - 1) / (wg / 4)) * (wg / 64));
     std::vector<unsigned long long> pr((size_t)waves * 16);
     // warm up in bench.py's order (protect, unprotect alternating)
