@@ -61,7 +61,8 @@ int main(int argc, char **argv)
 #else
     if (n == 0) return 2;
 #endif
-    const int hdr = 11, payload = 1173, slot = 1200;
+    // header length (argv[4], default 11): 16 puts every ciphertext block on a 16-byte boundary
+    const int hdr = argc > 4 ? atoi(argv[4]) : 11, slot = 1200, payload = slot - 16 - hdr;
     qpp_keytab *kt = nullptr;
     if (qpp_keytab_create(4, &kt) != QPP_OK) { printf("keytab failed\n"); return 1; }
     qpp_key_material km = {};
@@ -77,8 +78,8 @@ int main(int argc, char **argv)
     std::vector<qpp_desc> pd(n), ud(n);
     for (uint32_t i = 0; i < n; ++i) {
         h_in[(size_t)i * slot] = 0x41;  // short header, 2-byte packet number = i
-        h_in[(size_t)i * slot + 9] = (uint8_t)(i >> 8);
-        h_in[(size_t)i * slot + 10] = (uint8_t)i;
+        h_in[(size_t)i * slot + hdr - 2] = (uint8_t)(i >> 8);
+        h_in[(size_t)i * slot + hdr - 1] = (uint8_t)i;
         pd[i] = qpp_desc{(uint64_t)i * slot, (uint64_t)i * slot, (uint32_t)payload, (uint16_t)hdr, 0,
                          i, 0, 0};
         ud[i] = qpp_desc{(uint64_t)i * slot, (uint64_t)i * slot, (uint32_t)slot, (uint16_t)(hdr - 2),
