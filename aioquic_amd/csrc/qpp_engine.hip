@@ -55,6 +55,9 @@ constexpr bool kBalanceEnc = QPP_BALANCE_ENC;  // ... for protect too
 #ifndef QPP_VMCNT1
 #define QPP_VMCNT1 0  // GCM step loop: wait for the LDS-DMA only, not the last store (no gain)
 #endif
+#ifndef QPP_STORE_CPOL
+#define QPP_STORE_CPOL 0  // cache policy of the GCM step stores (gfx950: 1 sc0, 2 nt, 16 sc1)
+#endif
 #ifndef QPP_CHACHA_WPE
 #define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget)
 #endif
@@ -534,7 +537,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
             *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
         }
-        __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
         acc ^= x;
 #if !QPP_FUSE_GH
         __builtin_amdgcn_sched_barrier(0);
