@@ -13,6 +13,7 @@ Other configs (--config 3/4/5) are parity/throughput cases of the same path.
 """
 
 import argparse
+import ctypes
 import glob
 import importlib.util
 import json
@@ -49,8 +50,9 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=100,
+                    help="untimed steps first: about 20 ms of work, which the GPU clock needs to ramp")
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -174,6 +176,58 @@ def cpu_baseline(w, seconds: float, cfg, procs: int = 1):
 # --------------------------------------------------------------------- main --
 
 
+class HipEvents:
+    """Timing-only HIP events on torch's HIP runtime, created with
+    hipEventReleaseToDevice (or hipEventDisableSystemFence; hip_runtime_api.h)
+    so that recording one does not write back and invalidate the caches the
+    way a default event does (each default event costs ~15 us of stream time
+    here).  `flags` records which one the runtime accepted."""
+
+    # preferred first; the runtime may refuse a combination
+    FLAG_CHOICES = (0x40000000, 0x20000000, 0x0)  # ReleaseToDevice, DisableSystemFence, default
+
+    def __init__(self, torch):
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        self.hip = hip = ctypes.CDLL(lib)  # the copy torch already loaded
+        vp = ctypes.c_void_p
+        hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
+        hip.hipEventRecord.argtypes = [vp, vp]
+        hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+        hip.hipEventDestroy.argtypes = [vp]
+        self.events = []
+        self.flags = None
+        for f in self.FLAG_CHOICES:
+            e = ctypes.c_void_p()
+            if hip.hipEventCreateWithFlags(ctypes.byref(e), f) == 0:
+                hip.hipEventDestroy(e)
+                self.flags = f
+                break
+        if self.flags is None:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+
+    def new(self):
+        e = ctypes.c_void_p()
+        if self.hip.hipEventCreateWithFlags(ctypes.byref(e), self.flags) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+        self.events.append(e)
+        return e
+
+    def record(self, e, stream) -> None:
+        if self.hip.hipEventRecord(e, ctypes.c_void_p(int(stream.cuda_stream))) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def ms(self, a, b) -> float:
+        out = ctypes.c_float()
+        if self.hip.hipEventElapsedTime(ctypes.byref(out), a, b) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return float(out.value)
+
+    def close(self) -> None:
+        for e in self.events:
+            self.hip.hipEventDestroy(e)
+        self.events = []
+
+
 def hbm_copy_gbs(dev, nbytes=1 << 30, reps=10):
     """Attainable HBM bandwidth on this box: a device-to-device copy of 1 GiB
     (read + write bytes / time), the practical ceiling beside the 8 TB/s spec."""
@@ -277,22 +331,31 @@ def main():
     d_r2 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def step():
+    hev = HipEvents(torch)
+
+    def step(ev=None):
+        if ev:
+            hev.record(ev[0], stream)
         eng.protect(d_desc, n, d_plain, d_wire, d_r1, stream)
+        if ev:
+            hev.record(ev[1], stream)
         eng.unprotect(d_udesc, n, d_wire, d_back, d_r2, stream)
+        if ev:
+            hev.record(ev[2], stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
 
-    # the timed region: K steps back to back on the stream, no event packets
-    # between the kernels (each costs ~15 us of stream time on this stack)
+    # the timed region: K steps on one stream, each kernel between two
+    # timing-only HIP events (its launch duration for the roofline)
+    evs = [[hev.new() for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step()
+        step(evs[k])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -302,22 +365,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # Launch duration of each kernel: `reps` back-to-back launches between two
-    # HIP events on the launch stream (events around every launch would add
-    # their own stream time to each).  Protect rewrites the same wire bytes and
-    # unprotect the same plaintext.
-    def back_to_back(fn, reps=20):
-        fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            fn()
-        e1.record(stream)
-        e1.synchronize()
-        return e0.elapsed_time(e1) / 1e3 / reps
-
-    b_prot = back_to_back(lambda: eng.protect(d_desc, n, d_plain, d_wire, d_r1, stream))
-    b_unp = back_to_back(lambda: eng.unprotect(d_udesc, n, d_wire, d_back, d_r2, stream))
+    t_prot = float(np.mean([hev.ms(e[0], e[1]) for e in evs])) / 1e3
+    t_unp = float(np.mean([hev.ms(e[1], e[2]) for e in evs])) / 1e3
+    hev_flags = hev.flags
+    hev.close()
 
     # every packet of the last step must authenticate (cheap, after timing)
     r1 = d_r1.cpu().numpy().view(L.RESULT)
@@ -329,8 +380,8 @@ def main():
     total_bytes = float(n) * 1200 * args.steps * world
     value = total_bytes / elapsed / GIB
     copy_gbs = hbm_copy_gbs(dev) if rank == 0 else None
-    kern_t = max(b_prot, b_unp)
-    dom = "protect" if b_prot >= b_unp else "unprotect"
+    kern_t = max(t_prot, t_unp)
+    dom = "protect" if t_prot >= t_unp else "unprotect"
     achieved = BYTES_PER_PKT_KERNEL * n / kern_t / 1e9
     traffic = measured_traffic(cfg["name"], n, dom)
     floor = None
@@ -358,8 +409,9 @@ def main():
             "data": "synthetic (seeded 1-RTT packets, 11 B header + 1173 B payload + 16 B tag)",
             "config": {"workload": cfg["name"], "packets_per_gpu": n, "packet_bytes": 1200,
                        "keys": w.n_keys, "parallelism": f"packet shards x{world}"},
-            "kernels_ms": {"protect": round(b_prot * 1e3, 4), "unprotect": round(b_unp * 1e3, 4)},
-            "kernel_gib_s": round(n * 1200 / (b_prot + b_unp) / GIB, 3),
+            "kernels_ms": {"protect": round(t_prot * 1e3, 4), "unprotect": round(t_unp * 1e3, 4)},
+            "kernel_gib_s": round(n * 1200 / (t_prot + t_unp) / GIB, 3),
+            "event_flags": hex(hev_flags),
             "roofline": {"bound": "hbm", "kernel": dom, "launch_us": round(kern_t * 1e6, 2),
                          "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
