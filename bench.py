@@ -62,8 +62,11 @@ def parse():
     ap.add_argument("--e2e", action="store_true", help="also time pinned H2D->kernels->D2H")
     ap.add_argument("--e2e-packets", type=int, default=1 << 20,
                     help="packets of the end-to-end run (the north star's 1Mi)")
-    ap.add_argument("--e2e-chunks", type=int, default=16)
+    ap.add_argument("--e2e-chunks", type=int, default=32)
     ap.add_argument("--e2e-streams", type=int, default=4)
+    ap.add_argument("--e2e-mode", choices=("staged", "per-chunk"), default="staged",
+                    help="staged: one H2D, one compute and one D2H stream chained by events; "
+                         "per-chunk: each chunk's copy/kernels/copy on one of --e2e-streams streams")
     ap.add_argument("--check", action="store_true", help="verify round trip after timing")
     return ap.parse_args()
 
@@ -430,18 +433,25 @@ def main():
             out["key_schedule"] = key_schedule(PacketEngine, w.n_keys, cfg["suite"], cfg["version"])
         if args.e2e:
             out["e2e"] = e2e(PacketEngine, cfg, 0x9001 + args.config, dev, args.e2e_packets,
-                             chunks=args.e2e_chunks, n_streams=args.e2e_streams)
+                             chunks=args.e2e_chunks, n_streams=args.e2e_streams,
+                             mode=args.e2e_mode)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5):
-    """Pinned host -> H2D -> protect -> unprotect -> D2H, pipelined over
-    `n_streams` streams in `chunks` slices (the path starts and ends in UDP
-    socket buffers), on its own workload of `n` packets (the north star's
-    1Mi x 1200 B by default).  Verifies the round trip."""
+def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5, mode="staged"):
+    """Pinned host -> H2D -> protect -> unprotect -> D2H in `chunks` slices
+    (the path starts and ends in UDP socket buffers), on its own workload of
+    `n` packets (the north star's 1Mi x 1200 B by default).  Verifies the
+    round trip.
+
+    mode "staged": a three-stage pipeline -- every H2D on one copy stream,
+    every kernel pair on one compute stream, every D2H on a second copy
+    stream, each chunk handed on by an event -- so the two PCIe directions
+    and the kernels of three different chunks run at once.
+    mode "per-chunk": chunk c's four steps in order on stream c % n_streams."""
     import torch
     from aioquic_amd.bench_data import make_workload
 
@@ -465,18 +475,36 @@ def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5):
         udescs.append(torch.from_numpy(u.view(np.uint8)).to(dev))
         res.append(torch.empty(per * 16, dtype=torch.uint8, device=dev))
     span = per * 1200
+    stages = [torch.cuda.Stream(dev) for _ in range(3)]
+    ev_in = [torch.cuda.Event() for _ in range(chunks)]
+    ev_k = [torch.cuda.Event() for _ in range(chunks)]
     times = []
     for _ in range(reps):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for c in range(chunks):
-            s = streams[c % n_streams]
-            with torch.cuda.stream(s):
+        if mode == "staged":
+            s_in, s_k, s_out = stages
+            for c in range(chunks):
                 lo, hi = c * span, (c + 1) * span
-                d_in[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
-                eng.protect(descs[c], per, d_in, d_wire, res[c], s)
-                eng.unprotect(udescs[c], per, d_wire, d_out, res[c], s)
-                h_out[lo:hi].copy_(d_out[lo:hi], non_blocking=True)
+                with torch.cuda.stream(s_in):
+                    d_in[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
+                    ev_in[c].record(s_in)
+                s_k.wait_event(ev_in[c])
+                eng.protect(descs[c], per, d_in, d_wire, res[c], s_k)
+                eng.unprotect(udescs[c], per, d_wire, d_out, res[c], s_k)
+                ev_k[c].record(s_k)
+                s_out.wait_event(ev_k[c])
+                with torch.cuda.stream(s_out):
+                    h_out[lo:hi].copy_(d_out[lo:hi], non_blocking=True)
+        else:
+            for c in range(chunks):
+                s = streams[c % n_streams]
+                with torch.cuda.stream(s):
+                    lo, hi = c * span, (c + 1) * span
+                    d_in[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
+                    eng.protect(descs[c], per, d_in, d_wire, res[c], s)
+                    eng.unprotect(udescs[c], per, d_wire, d_out, res[c], s)
+                    h_out[lo:hi].copy_(d_out[lo:hi], non_blocking=True)
         torch.cuda.synchronize(dev)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
@@ -502,9 +530,11 @@ def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5):
     ok = bool(np.array_equal(h_out.numpy()[: per * chunks * 1200], w.plain[: per * chunks * 1200]))
     return {"gib_s": round(per * chunks * 1200 / t / GIB, 3), "packets": per * chunks,
             "round_trip_ok": ok, "chunks": chunks,
-            "streams": n_streams, "h2d_gib_s": leg["h2d"], "d2h_gib_s": leg["d2h"],
+            "streams": 3 if mode == "staged" else n_streams, "mode": mode, "h2d_gib_s": leg["h2d"], "d2h_gib_s": leg["d2h"],
             "duplex_gib_s_each_way": leg["duplex"],
-            "note": f"pinned H2D + protect + unprotect + D2H, {n_streams} streams"}
+            "note": ("pinned H2D + protect + unprotect + D2H, "
+                     + ("3-stage pipeline (H2D / kernels / D2H streams)" if mode == "staged"
+                        else f"{n_streams} streams, one chunk per stream"))}
 
 
 if __name__ == "__main__":
