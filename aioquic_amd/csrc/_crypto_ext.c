@@ -523,7 +523,9 @@ static PyObject *batch_host(PyObject *args, int enc)
     out = PyBytes_FromStringAndSize(NULL, out_len);
     res = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_result));
     if (!out || !res) goto done;
-    memset(PyBytes_AS_STRING(out), 0, (size_t)out_len);
+    /* the session writes every byte of out (zeros where no packet lands) for
+       n > 0, so only an empty batch needs the zero fill here */
+    if (n == 0) memset(PyBytes_AS_STRING(out), 0, (size_t)out_len);
     int rc;
     Py_BEGIN_ALLOW_THREADS
     rc = enc ? qpp_session_protect(g_session, kt, desc.buf, n, data.buf, (size_t)data.len,

@@ -1153,6 +1153,8 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 #include <stdlib.h>
 #include <string.h>
 
+#include <thread>
+
 using namespace qpp;
 
 struct qpp_keytab {
@@ -1165,8 +1167,16 @@ struct qpp_keytab {
     uint32_t suite_mask;  // bit s set once a slot of suite s was installed
 };
 
+// Host batches of at least 2 x kPipeChunkBytes of output go through the
+// session as a three-stage pipeline of up to kPipeMaxChunks chunks (see
+// session_run_pipelined).
+constexpr size_t kPipeChunkBytes = (size_t)32 << 20;
+constexpr int kPipeMaxChunks = 32;
+
 struct qpp_session {
-    hipStream_t stream;
+    hipStream_t stream;             // kernels (and everything of the serial path)
+    hipStream_t s_in, s_out;        // pipelined path: H2D and D2H copy streams
+    hipEvent_t ev_in[kPipeMaxChunks], ev_k[kPipeMaxChunks], ev_out[kPipeMaxChunks];
     int device;
     size_t max_bytes;
     uint32_t max_packets;
@@ -1468,6 +1478,17 @@ int qpp_session_create(size_t max_bytes, uint32_t max_packets, qpp_session **out
         free(s);
         return QPP_E_HIP;
     }
+    bool ok = hipStreamCreateWithFlags(&s->s_in, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&s->s_out, hipStreamNonBlocking) == hipSuccess;
+    for (int c = 0; ok && c < kPipeMaxChunks; ++c)
+        ok = hipEventCreateWithFlags(&s->ev_in[c], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&s->ev_k[c], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&s->ev_out[c], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        qpp_session_destroy(s);
+        return QPP_E_HIP;
+    }
     rc = session_reserve(s, max_bytes, max_packets);
     if (rc != QPP_OK) {
         qpp_session_destroy(s);
@@ -1481,12 +1502,132 @@ void qpp_session_destroy(qpp_session *s)
 {
     if (!s) return;
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->s_in) (void)hipStreamSynchronize(s->s_in);
+    if (s->s_out) (void)hipStreamSynchronize(s->s_out);
     session_free_buffers(s);
+    for (int c = 0; c < kPipeMaxChunks; ++c) {
+        if (s->ev_in[c]) (void)hipEventDestroy(s->ev_in[c]);
+        if (s->ev_k[c]) (void)hipEventDestroy(s->ev_k[c]);
+        if (s->ev_out[c]) (void)hipEventDestroy(s->ev_out[c]);
+    }
+    if (s->s_in) (void)hipStreamDestroy(s->s_in);
+    if (s->s_out) (void)hipStreamDestroy(s->s_out);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     free(s);
 }
 
 void *qpp_session_stream(qpp_session *s) { return s ? (void *)s->stream : NULL; }
+
+// Large host batches: chunk c of the packets (in descriptor order) is copied
+// into pinned staging by the host and sent H2D on s_in, processed on the
+// kernel stream once its input event fires, and returned D2H on s_out once its
+// kernel event fires; the host copies chunk c out while later chunks are still
+// in flight.  The host memcpys, both PCIe directions and the kernels of
+// different chunks overlap.  Requires out_off non-decreasing in descriptor
+// order: chunk c's D2H then covers [out_off of its first packet, out_off of
+// the next chunk's first packet) -- chunk 0 from 0, the last chunk to out_len
+// -- so the chunks tile the output, and bytes a packet writes past its tile
+// are copied by a later chunk's D2H, which runs after this chunk's kernel.
+// Each chunk's H2D covers the input extent of its own packets (over-copying
+// bytes of a neighbour is harmless: same host bytes).
+// Host copies between caller memory and pinned staging: one thread streams
+// ~10 GB/s, well under the PCIe rate, so large copies are split over threads.
+static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
+{
+    constexpr size_t kPart = (size_t)4 << 20;
+    constexpr int kMaxThreads = 8;
+    int parts = (int)(bytes / kPart);
+    if (parts > kMaxThreads) parts = kMaxThreads;
+    if (parts < 2) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    std::thread th[kMaxThreads];
+    const size_t step = (bytes / parts + 63) & ~(size_t)63;
+    for (int t = 1; t < parts; ++t) {
+        const size_t lo = step * t;
+        if (lo >= bytes) break;
+        const size_t len = lo + step < bytes && t + 1 < parts ? step : bytes - lo;
+        th[t] = std::thread([=] { memcpy(dst + lo, src + lo, len); });
+    }
+    memcpy(dst, src, step < bytes ? step : bytes);
+    for (int t = 1; t < parts; ++t)
+        if (th[t].joinable()) th[t].join();
+}
+
+static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
+                                 const qpp_desc *desc, uint32_t n, const uint8_t *in,
+                                 size_t in_len, uint8_t *out, size_t out_len, qpp_result *res,
+                                 int chunks)
+{
+    qpp_desc *hd = (qpp_desc *)s->h_misc;
+    qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
+    qpp_desc *dd = (qpp_desc *)s->d_misc;
+    qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
+    memcpy(hd, desc, (size_t)n * sizeof(qpp_desc));
+    HIPCHK(hipMemcpyAsync(dd, hd, (size_t)n * sizeof(qpp_desc), hipMemcpyHostToDevice, s->s_in));
+    HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
+    size_t olo[kPipeMaxChunks + 1];
+    uint32_t first[kPipeMaxChunks + 1];
+    for (int c = 0; c <= chunks; ++c) {
+        first[c] = (uint32_t)((uint64_t)n * c / chunks);
+        olo[c] = c == 0 ? 0 : c == chunks ? out_len : (size_t)desc[first[c]].out_off;
+        if (olo[c] > out_len) olo[c] = out_len;
+    }
+    int rc = QPP_OK;
+    int next_out = 0;
+    for (int c = 0; c < chunks; ++c) {
+        const uint32_t a = first[c], b = first[c + 1];
+        size_t lo = SIZE_MAX, hi = 0;
+        for (uint32_t i = a; i < b; ++i) {
+            const size_t o = (size_t)desc[i].in_off;
+            const size_t e = o + (size_t)desc[i].hdr_len + desc[i].len + 16;
+            if (o < lo) lo = o;
+            if (e > hi) hi = e;
+        }
+        if (hi > in_len) hi = in_len;
+        if (lo < hi) {
+            par_memcpy(s->h_in + lo, in + lo, hi - lo);
+            HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice,
+                                  s->s_in));
+        }
+        HIPCHK(hipEventRecord(s->ev_in[c], s->s_in));
+        HIPCHK(hipStreamWaitEvent(s->stream, s->ev_in[c], 0));
+        if (b > a) {
+            rc = launch_packets(enc, kt, dd + a, b - a, s->d_in, s->d_out, dr + a, s->stream);
+            if (rc != QPP_OK) break;
+        }
+        HIPCHK(hipEventRecord(s->ev_k[c], s->stream));
+        HIPCHK(hipStreamWaitEvent(s->s_out, s->ev_k[c], 0));
+        if (olo[c + 1] > olo[c])
+            HIPCHK(hipMemcpyAsync(s->h_out + olo[c], s->d_out + olo[c], olo[c + 1] - olo[c],
+                                  hipMemcpyDeviceToHost, s->s_out));
+        HIPCHK(hipEventRecord(s->ev_out[c], s->s_out));
+        // hand back chunks whose D2H has already landed while later ones fly
+        while (next_out < c) {
+            if (hipEventQuery(s->ev_out[next_out]) != hipSuccess) {
+                (void)hipGetLastError();  // hipErrorNotReady must not reach a later HIPCHK
+                break;
+            }
+            const int d = next_out++;
+            if (olo[d + 1] > olo[d]) par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d]);
+        }
+    }
+    if (rc != QPP_OK) {
+        (void)hipStreamSynchronize(s->s_in);
+        (void)hipStreamSynchronize(s->stream);
+        (void)hipStreamSynchronize(s->s_out);
+        return rc;
+    }
+    HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->s_out));
+    for (int c = next_out; c < chunks; ++c) {
+        HIPCHK(hipEventSynchronize(s->ev_out[c]));
+        if (olo[c + 1] > olo[c]) par_memcpy(out + olo[c], s->h_out + olo[c], olo[c + 1] - olo[c]);
+    }
+    HIPCHK(hipStreamSynchronize(s->s_out));
+    memcpy(res, hr, (size_t)n * sizeof(qpp_result));
+    return QPP_OK;
+}
 
 static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc,
                        uint32_t n, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len,
@@ -1497,6 +1638,17 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
     size_t need = in_len > out_len ? in_len : out_len;
     int rc = session_reserve(s, need, n);
     if (rc != QPP_OK) return rc;
+    size_t want = out_len / kPipeChunkBytes;
+    int chunks = want > (size_t)kPipeMaxChunks ? kPipeMaxChunks : (int)want;
+    if (chunks > (int)n) chunks = (int)n;
+    const char *serial = getenv("QPP_SESSION_SERIAL");  // A/B switch: "1" = serial path
+    if (chunks >= 2 && !(serial && serial[0] == '1')) {
+        bool mono = true;
+        for (uint32_t i = 1; i < n && mono; ++i) mono = desc[i].out_off >= desc[i - 1].out_off;
+        if (mono)
+            return session_run_pipelined(enc, s, kt, desc, n, in, in_len, out, out_len, res,
+                                         chunks);
+    }
     qpp_desc *hd = (qpp_desc *)s->h_misc;
     qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     qpp_desc *dd = (qpp_desc *)s->d_misc;

@@ -459,3 +459,64 @@ def test_fused_protect_length_boundary(oracle, L, engine_cls):
     assert len(hp.apply(b"\x40" + bytes(10), bytes(1489))) == 1500
     with pytest.raises(CryptoError, match="Invalid payload length"):
         hp.apply(b"\x40" + bytes(10), bytes(1490))
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_session_pipelined_host_batch(L, engine_cls, mixed):
+    """Host-buffer batches of >= 64 MiB go through the session's three-stage
+    pipeline (chunked H2D / kernels / D2H, qpp_engine.hip session_run_pipelined).
+    Its output and results must equal the serial session path
+    (QPP_SESSION_SERIAL=1) and the device-resident path byte for byte; a
+    tampered packet in a late chunk reports its status in place; a
+    non-monotone descriptor order (serial fallback) gives the same bytes."""
+    import torch
+
+    from aioquic_amd import bench_data
+
+    n = 98304  # 118 MB of wire: 3 pipeline chunks
+    kw = dict(mixed=[0, 2]) if mixed else {}
+    w = bench_data.make_workload(n, suite=0, n_keys=7, seed=0x51 + int(mixed), **kw)
+    eng = engine_cls(w.n_keys)
+    eng.set_key_records(w.keys)
+    plain = w.plain.tobytes()
+    out_p, res_p = eng.protect_host(w.desc, plain, w.wire_size)
+    os.environ["QPP_SESSION_SERIAL"] = "1"
+    try:
+        out_s, res_s = eng.protect_host(w.desc, plain, w.wire_size)
+    finally:
+        del os.environ["QPP_SESSION_SERIAL"]
+    assert np.array_equal(out_p, out_s)
+    assert res_p.tobytes() == res_s.tobytes()
+    assert (res_p["status"] == L.S_OK).all()
+    dev = torch.device("cuda")
+    d_wire = torch.zeros(w.wire_size, dtype=torch.uint8, device=dev)
+    d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    eng.protect(torch.from_numpy(w.desc.view(np.uint8)).to(dev), n,
+                torch.from_numpy(w.plain).to(dev), d_wire, d_res)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_wire.cpu().numpy(), out_p)
+    # unprotect through the pipeline, one packet of the last chunk tampered
+    wire = out_p.copy()
+    bad = n - 5
+    wire[int(w.udesc[bad]["in_off"]) + 600] ^= 1
+    back, r = eng.unprotect_host(w.udesc, wire.tobytes(), w.plain_size)
+    assert r["status"][bad] == L.S_DECRYPT
+    ok = np.ones(n, bool)
+    ok[bad] = False
+    assert (r["status"][ok] == L.S_OK).all()
+    assert (r["pn"][ok] == w.udesc["pn"][ok]).all()
+    for i in (0, 1, n // 3, n // 2, n - 6, n - 1):
+        o = int(w.udesc[i]["out_off"])
+        ln = int(r["hdr_len"][i]) + int(r["out_len"][i])
+        assert np.array_equal(back[o : o + ln], w.plain[o : o + ln])
+    plain_ok = back.copy()
+    po = int(w.udesc[bad]["out_off"])
+    plain_ok[po : po + 1200] = 0
+    ref = w.plain.copy()
+    ref[po : po + 1200] = 0
+    assert np.array_equal(plain_ok, ref)
+    # reversed descriptor order: not monotone, served by the serial path
+    rev = w.desc[::-1].copy()
+    out_r, res_r = eng.protect_host(rev, plain, w.wire_size)
+    assert np.array_equal(out_r, out_p)
+    assert res_r.tobytes() == res_p[::-1].tobytes()
