@@ -151,7 +151,10 @@ int qpp_hp_mask(const qpp_keytab *kt, const uint32_t *d_slots, const uint8_t *d_
                 uint32_t n, uint8_t *d_masks, void *stream);
 
 /* Synchronous host-buffer forms (pinned staging, H2D, kernel, D2H), used by the
- * per-packet object API and the end-to-end measurement. */
+ * per-packet object API and the batched send/receive callers.  A batch with at
+ * least 64 MiB of output and out_off non-decreasing in descriptor order runs as
+ * a chunked H2D / kernel / D2H pipeline on three streams (QPP_SESSION_SERIAL=1
+ * in the environment forces the serial form); the bytes written are the same. */
 int qpp_session_create(size_t max_bytes, uint32_t max_packets, qpp_session **out);
 void qpp_session_destroy(qpp_session *s);
 void *qpp_session_stream(qpp_session *s);
