@@ -410,7 +410,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded 1-RTT packets, 11 B header + 1173 B payload + 16 B tag)",
-            "config": {"workload": cfg["name"], "packets_per_gpu": n, "packet_bytes": 1200,
+            "config": {"workload": _workload_name(cfg, n), "packets_per_gpu": n, "packet_bytes": 1200,
                        "keys": w.n_keys, "parallelism": f"packet shards x{world}"},
             "kernels_ms": {"protect": round(t_prot * 1e3, 4), "unprotect": round(t_unp * 1e3, 4)},
             "kernel_gib_s": round(n * 1200 / (t_prot + t_unp) / GIB, 3),
@@ -439,6 +439,15 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _workload_name(cfg, n):
+    """cfg's name, with the packet count replaced when --packets overrides it."""
+    if n == cfg["n"]:
+        return cfg["name"]
+    def ki(x):
+        return f"{x >> 20}Mi" if x % (1 << 20) == 0 else f"{x >> 10}Ki" if x % 1024 == 0 else str(x)
+    return cfg["name"].replace(ki(cfg["n"]), ki(n), 1)
 
 
 def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5, mode="staged"):
