@@ -1613,12 +1613,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
             if (olo[d + 1] > olo[d]) par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d]);
         }
     }
-    if (rc != QPP_OK) {
-        (void)hipStreamSynchronize(s->s_in);
-        (void)hipStreamSynchronize(s->stream);
-        (void)hipStreamSynchronize(s->s_out);
-        return rc;
-    }
+    if (rc != QPP_OK) return rc;
     HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->s_out));
     for (int c = next_out; c < chunks; ++c) {
         HIPCHK(hipEventSynchronize(s->ev_out[c]));
@@ -1627,6 +1622,19 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     HIPCHK(hipStreamSynchronize(s->s_out));
     memcpy(res, hr, (size_t)n * sizeof(qpp_result));
     return QPP_OK;
+}
+
+// On a failure, drain the session's streams before returning, so no copy into
+// its staging is still in flight when the staging is reused or freed.
+static int session_drain_on_error(qpp_session *s, int rc)
+{
+    if (rc != QPP_OK && s) {
+        if (s->s_in) (void)hipStreamSynchronize(s->s_in);
+        (void)hipStreamSynchronize(s->stream);
+        if (s->s_out) (void)hipStreamSynchronize(s->s_out);
+        (void)hipGetLastError();
+    }
+    return rc;
 }
 
 static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc,
@@ -1673,14 +1681,14 @@ int qpp_session_protect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *de
                         const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len,
                         qpp_result *res)
 {
-    return session_run(true, s, kt, desc, n, in, in_len, out, out_len, res);
+    return session_drain_on_error(s, session_run(true, s, kt, desc, n, in, in_len, out, out_len, res));
 }
 
 int qpp_session_unprotect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc,
                           uint32_t n, const uint8_t *in, size_t in_len, uint8_t *out,
                           size_t out_len, qpp_result *res)
 {
-    return session_run(false, s, kt, desc, n, in, in_len, out, out_len, res);
+    return session_drain_on_error(s, session_run(false, s, kt, desc, n, in, in_len, out, out_len, res));
 }
 
 int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *slots,
