@@ -317,6 +317,10 @@ def main():
         if args.cpu_all_cores:
             cpu_all = cpu_baseline(w, max(2.0, args.cpu_seconds / 2), cfg, cpu_share())
 
+    # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box)
+    # share devices round-robin
+    ndev = torch.cuda.device_count()
+    local = local % ndev if ndev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
