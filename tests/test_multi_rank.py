@@ -102,3 +102,13 @@ def test_shard_protect_matches_oracle_per_rank(oracle):
         assert (res2["status"] == 0).all()
         v = back.reshape(n, 1200)[:, :1184]
         assert np.array_equal(v, w.plain.reshape(n, 1200)[:, :1184])
+
+
+def test_bench_workload_label_follows_packet_override():
+    """bench.py names the packet count it ran, not only the config's default."""
+    import bench
+
+    c2 = bench.CONFIGS[2]
+    assert bench._workload_name(c2, c2["n"]) == c2["name"]
+    assert bench._workload_name(c2, 1 << 20) == "aes-128-gcm 1Mi x 1200B, 1 key"
+    assert bench._workload_name(c2, 1 << 17) == "aes-128-gcm 128Ki x 1200B, 1 key"
