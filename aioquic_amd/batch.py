@@ -101,6 +101,15 @@ class PacketEngine:
         return np.frombuffer(out, dtype=np.uint8), np.frombuffer(res, dtype=L.RESULT)
 
 
+    def protect_into(self, desc: np.ndarray, data, out: np.ndarray, results: np.ndarray) -> None:
+        """protect_host into caller-owned buffers (out: uint8, results: RESULT
+        array of len(desc)), reusable across batches."""
+        _crypto.protect_into(self.table, np.ascontiguousarray(desc), data, out, results)
+
+    def unprotect_into(self, desc: np.ndarray, data, out: np.ndarray, results: np.ndarray) -> None:
+        _crypto.unprotect_into(self.table, np.ascontiguousarray(desc), data, out, results)
+
+
 def layout_packets(headers, payloads, pns, slots, *, align: int = 1, tag_room: bool = True,
                    flags: int = 0):
     """Pack (header, payload) pairs into one input buffer and build protect

@@ -545,6 +545,49 @@ done:
     return ret;
 }
 
+/* protect_into / unprotect_into(table, desc, data, out, results): the host
+   form with caller-owned, writable output and result buffers (any buffer
+   object, e.g. a numpy array reused across batches), so a large batch does
+   not allocate and first-touch a fresh bytes object per call. */
+static PyObject *batch_into(PyObject *args, int enc)
+{
+    PyObject *t;
+    Py_buffer desc, data, out, res;
+    if (!PyArg_ParseTuple(args, "Oy*y*w*w*", &t, &desc, &data, &out, &res)) return NULL;
+    PyObject *ret = NULL;
+    qpp_keytab *kt = as_table(t);
+    if (!kt || !session()) goto done;
+    if (desc.len % (Py_ssize_t)sizeof(qpp_desc)) {
+        PyErr_SetString(PyExc_ValueError, "bad descriptor buffer");
+        goto done;
+    }
+    uint32_t n = (uint32_t)(desc.len / (Py_ssize_t)sizeof(qpp_desc));
+    if (res.len < (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_result)) {
+        PyErr_SetString(PyExc_ValueError, "results buffer too small");
+        goto done;
+    }
+    if (n == 0) memset(out.buf, 0, (size_t)out.len);
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = enc ? qpp_session_protect(g_session, kt, desc.buf, n, data.buf, (size_t)data.len,
+                                   (uint8_t *)out.buf, (size_t)out.len, (qpp_result *)res.buf)
+             : qpp_session_unprotect(g_session, kt, desc.buf, n, data.buf, (size_t)data.len,
+                                     (uint8_t *)out.buf, (size_t)out.len, (qpp_result *)res.buf);
+    Py_END_ALLOW_THREADS
+    if (check_rc(rc) < 0) goto done;
+    ret = Py_None;
+    Py_INCREF(ret);
+done:
+    PyBuffer_Release(&desc);
+    PyBuffer_Release(&data);
+    PyBuffer_Release(&out);
+    PyBuffer_Release(&res);
+    return ret;
+}
+
+static PyObject *py_protect_into(PyObject *m, PyObject *args) { return batch_into(args, 1); }
+static PyObject *py_unprotect_into(PyObject *m, PyObject *args) { return batch_into(args, 0); }
+
 static PyObject *py_protect_host(PyObject *m, PyObject *args) { return batch_host(args, 1); }
 static PyObject *py_unprotect_host(PyObject *m, PyObject *args) { return batch_host(args, 0); }
 
@@ -586,6 +629,8 @@ static PyMethodDef module_methods[] = {
     {"unprotect", py_unprotect, METH_VARARGS, "unprotect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream)"},
     {"protect_host", py_protect_host, METH_VARARGS, "protect_host(table, desc, data, out_len) -> (out, results)"},
     {"unprotect_host", py_unprotect_host, METH_VARARGS, "unprotect_host(table, desc, data, out_len) -> (out, results)"},
+    {"protect_into", py_protect_into, METH_VARARGS, "protect_into(table, desc, data, out, results) -> None"},
+    {"unprotect_into", py_unprotect_into, METH_VARARGS, "unprotect_into(table, desc, data, out, results) -> None"},
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},

@@ -487,6 +487,12 @@ def test_session_pipelined_host_batch(L, engine_cls, mixed):
         del os.environ["QPP_SESSION_SERIAL"]
     assert np.array_equal(out_p, out_s)
     assert res_p.tobytes() == res_s.tobytes()
+    # caller-owned, reused buffers (protect_into), stale contents overwritten
+    out_i = np.full(w.wire_size, 0xA5, np.uint8)
+    res_i = np.zeros(n, dtype=L.RESULT)
+    eng.protect_into(w.desc, w.plain, out_i, res_i)
+    assert np.array_equal(out_i, out_p)
+    assert res_i.tobytes() == res_p.tobytes()
     assert (res_p["status"] == L.S_OK).all()
     dev = torch.device("cuda")
     d_wire = torch.zeros(w.wire_size, dtype=torch.uint8, device=dev)
