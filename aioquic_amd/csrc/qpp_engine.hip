@@ -1535,9 +1535,14 @@ void *qpp_session_stream(qpp_session *s) { return s ? (void *)s->stream : NULL; 
 static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
 {
     constexpr size_t kPart = (size_t)4 << 20;
-    constexpr int kMaxThreads = 8;
+    constexpr int kMaxThreads = 16;
+    static const int max_threads = [] {
+        const char *v = getenv("QPP_COPY_THREADS");  // A/B switch, default 8
+        const int t = v ? atoi(v) : 8;
+        return t < 1 ? 1 : t > kMaxThreads ? kMaxThreads : t;
+    }();
     int parts = (int)(bytes / kPart);
-    if (parts > kMaxThreads) parts = kMaxThreads;
+    if (parts > max_threads) parts = max_threads;
     if (parts < 2) {
         memcpy(dst, src, bytes);
         return;
