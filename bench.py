@@ -59,6 +59,8 @@ def parse():
                     help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-all-cores", type=int, default=1,
                     help="also time the reference on every host core of this GPU's share")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="bracket the kernels of every N-th timed step with HIP events (1 = all)")
     ap.add_argument("--e2e", action="store_true", help="also time pinned H2D->kernels->D2H")
     ap.add_argument("--e2e-packets", type=int, default=1 << 20,
                     help="packets of the end-to-end run (the north star's 1Mi)")
@@ -354,9 +356,12 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    # the timed region: K steps on one stream, each kernel between two
-    # timing-only HIP events (its launch duration for the roofline)
-    evs = [[hev.new() for _ in range(3)] for _ in range(args.steps)]
+    # the timed region: K steps on one stream; in every `--event-every`-th step
+    # each kernel sits between two timing-only HIP events (its launch duration
+    # for the roofline).  Sampling keeps the events' own stream time (a few us
+    # per record) out of most steps of `value`.
+    every = max(1, args.event_every)
+    evs = [[hev.new() for _ in range(3)] if k % every == 0 else None for k in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -372,6 +377,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    evs = [e for e in evs if e]
     t_prot = float(np.mean([hev.ms(e[0], e[1]) for e in evs])) / 1e3
     t_unp = float(np.mean([hev.ms(e[1], e[2]) for e in evs])) / 1e3
     hev_flags = hev.flags
@@ -418,7 +424,7 @@ def main():
                        "keys": w.n_keys, "parallelism": f"packet shards x{world}"},
             "kernels_ms": {"protect": round(t_prot * 1e3, 4), "unprotect": round(t_unp * 1e3, 4)},
             "kernel_gib_s": round(n * 1200 / (t_prot + t_unp) / GIB, 3),
-            "event_flags": hex(hev_flags),
+            "event_flags": hex(hev_flags), "event_steps": len(evs),
             "roofline": {"bound": "hbm", "kernel": dom, "launch_us": round(kern_t * 1e6, 2),
                          "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
