@@ -44,10 +44,18 @@ class PacketEngine:
 
     Buffers are torch.uint8 CUDA tensors (or anything with ``data_ptr()``).
     Calls are asynchronous on ``stream`` (default: torch's current stream).
+
+    ``bucket(desc, n)`` sorts a batch by (suite, key slot) on the device
+    (qpp_plan_build); launches given ``plan=`` then run each suite over its
+    own bucket and write results in the caller's order.  A server batch that
+    interleaves connections wants this; a batch already grouped by key does
+    not need it.
     """
 
     def __init__(self, capacity: int):
         self.table = _crypto.KeyTable(int(capacity))
+        self._plan = None
+        self._plan_cap = 0
 
     @property
     def capacity(self) -> int:
@@ -80,13 +88,27 @@ class PacketEngine:
             return stream
         return int(stream.cuda_stream)
 
-    def protect(self, desc, n: int, inbuf, outbuf, results, stream=None) -> None:
-        _crypto.protect(self.table, _ptr(desc), int(n), _ptr(inbuf), _ptr(outbuf),
-                        _ptr(results), self._stream(stream))
+    def plan(self, n: int):
+        """The engine's bucketing scratch for batches of up to n packets."""
+        if self._plan is None or self._plan_cap < n:
+            self._plan = _crypto.Plan(max(int(n), 1))
+            self._plan_cap = max(int(n), 1)
+        return self._plan
 
-    def unprotect(self, desc, n: int, inbuf, outbuf, results, stream=None) -> None:
+    def bucket(self, desc, n: int, stream=None):
+        """Sort a device descriptor batch by (suite, slot); returns the plan
+        to pass to protect / unprotect of descriptors with the same slots."""
+        plan = self.plan(n)
+        _crypto.plan_build(plan, self.table, _ptr(desc), int(n), self._stream(stream))
+        return plan
+
+    def protect(self, desc, n: int, inbuf, outbuf, results, stream=None, plan=None) -> None:
+        _crypto.protect(self.table, _ptr(desc), int(n), _ptr(inbuf), _ptr(outbuf),
+                        _ptr(results), self._stream(stream), plan)
+
+    def unprotect(self, desc, n: int, inbuf, outbuf, results, stream=None, plan=None) -> None:
         _crypto.unprotect(self.table, _ptr(desc), int(n), _ptr(inbuf), _ptr(outbuf),
-                          _ptr(results), self._stream(stream))
+                          _ptr(results), self._stream(stream), plan)
 
     # ----------------------------------------------- host-buffer forms ----
 
@@ -104,10 +126,23 @@ class PacketEngine:
     def protect_into(self, desc: np.ndarray, data, out: np.ndarray, results: np.ndarray) -> None:
         """protect_host into caller-owned buffers (out: uint8, results: RESULT
         array of len(desc)), reusable across batches."""
-        _crypto.protect_into(self.table, np.ascontiguousarray(desc), data, out, results)
+        self._into(_crypto.protect_into, desc, data, out, results)
 
     def unprotect_into(self, desc: np.ndarray, data, out: np.ndarray, results: np.ndarray) -> None:
-        _crypto.unprotect_into(self.table, np.ascontiguousarray(desc), data, out, results)
+        self._into(_crypto.unprotect_into, desc, data, out, results)
+
+    def _into(self, fn, desc, data, out, results) -> None:
+        desc = np.ascontiguousarray(desc, dtype=L.DESC)
+        data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8)
+                                    if not isinstance(data, np.ndarray) else data.view(np.uint8).ravel())
+        if not (out.flags.c_contiguous and out.flags.writeable):
+            raise ValueError("out must be a writable contiguous array")
+        if not (results.flags.c_contiguous and results.flags.writeable) or \
+                results.nbytes < len(desc) * L.RESULT.itemsize:
+            raise ValueError("results must be a writable contiguous array of len(desc) records")
+        # the arrays stay referenced here for the whole call
+        fn(self.table, desc.ctypes.data, len(desc), data.ctypes.data, data.nbytes,
+           out.ctypes.data, out.nbytes, results.ctypes.data)
 
 
 def layout_packets(headers, payloads, pns, slots, *, align: int = 1, tag_room: bool = True,

@@ -329,9 +329,16 @@ class ReceiveBatch:
                     rolled = True
                 out, r, off = got
                 st = int(r["status"])
+                exp_now = it.space.expected_packet_number
+                if exp_now != exp_at[i] and st != L.S_OK:
+                    # decoded under an expected number an earlier packet has
+                    # since raised: the packet number, hence the nonce, may
+                    # differ now, so a failure is not final -- relaunch
+                    blocked.add(pid)
+                    stale.append(i)
+                    continue
                 if st == L.S_OK:
                     hl, ln, pn = int(r["hdr_len"]), int(r["out_len"]), int(r["pn"])
-                    exp_now = it.space.expected_packet_number
                     if exp_now != exp_at[i]:
                         pn_len = hl - it.pn_off
                         again = decode_packet_number(_signed_trunc(pn, pn_len), pn_len * 8, exp_now)

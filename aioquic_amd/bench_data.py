@@ -4,9 +4,15 @@ Packet = 1-RTT short header 0x41 | DCID(8, fixed) | PN16(pn) (11 B, the shape
 QuicPacketBuilder emits: packet_builder.py:19-20,230), plaintext 1173 B from a
 seeded PRNG, 16 B tag -> 1200 B on the wire (test_packet_builder.py:490-522).
 Secrets are seeded random 32 B (48 B for AES-256) expanded with
-derive_key_iv_hp semantics.  Packets are laid out one per 1200-byte slot;
-descriptors are grouped by key slot, which is how the engine's host side
-buckets a multi-connection batch before launch.
+derive_key_iv_hp semantics.  Packets are laid out one per 1200-byte slot in
+arrival order.  Arrival order is one of
+  "grouped"      packets of one key contiguous (a single connection's burst),
+  "round_robin"  packet i on key i mod n_keys,
+  "random"       every packet on a seeded random key -- what a server socket
+                 sees when many connections send at once
+                 (src/aioquic/asyncio/server.py:60-152); the engine buckets it
+                 by (suite, key) on the device (qpp_plan) before launch.
+Packet numbers count up per key in arrival order.
 """
 
 from __future__ import annotations
@@ -46,11 +52,14 @@ class Workload:
     suites: np.ndarray    # suite per packet
 
 
-def make_keys(n_keys: int, suites, seed: int, version: int) -> np.ndarray:
+def make_keys(n_keys: int, suites, seed: int, version: int, random_suites: bool = False) -> np.ndarray:
+    """Key slots 0..n_keys-1; suite of slot s = suites[s % len] or, with
+    random_suites, a seeded uniform pick among `suites`."""
     rng = np.random.default_rng(seed)
+    pick = np.random.default_rng(seed ^ 0x5EED).integers(0, len(suites), n_keys)
     recs = np.zeros(n_keys, dtype=L.KEY_MATERIAL)
     for s in range(n_keys):
-        suite = int(suites[s % len(suites)])
+        suite = int(suites[pick[s]] if random_suites else suites[s % len(suites)])
         secret = rng.bytes(48 if suite == L.AES_256_GCM else 32)
         key, iv, hp = derive_key_iv_hp(cipher_suite=_SUITE_TO_CS[suite], secret=secret,
                                        version=version)
@@ -62,20 +71,41 @@ def make_keys(n_keys: int, suites, seed: int, version: int) -> np.ndarray:
     return recs
 
 
+def _per_key_counter(key_of: np.ndarray, n_keys: int) -> np.ndarray:
+    """pn[i] = number of earlier packets on the same key (arrival order)."""
+    order = np.argsort(key_of, kind="stable")
+    counts = np.bincount(key_of, minlength=n_keys)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    rank = np.empty(len(key_of), np.int64)
+    rank[order] = np.arange(len(key_of)) - np.repeat(starts, counts)
+    return rank.astype(np.uint64)
+
+
 def make_workload(n: int, suite=L.AES_128_GCM, n_keys: int = 1, seed: int = 0x9001,
                   version: int = QuicProtocolVersion.VERSION_1, mixed=None,
-                  first_packet: int = 0) -> Workload:
-    """n packets; `mixed` = list of suites assigned to keys round-robin
-    (config 5), else every key uses `suite`."""
+                  first_packet: int = 0, order: str = "grouped") -> Workload:
+    """n packets; `mixed` = list of suites (config 5): keys get a seeded
+    random suite from it with order="random", else round-robin; without
+    `mixed` every key uses `suite`.  `first_packet` offsets a rank's shard
+    in the global stream."""
     suites = list(mixed) if mixed else [suite]
-    keys = make_keys(n_keys, suites, seed, int(version))
+    keys = make_keys(n_keys, suites, seed, int(version), random_suites=order == "random")
     rng = np.random.default_rng(seed + 1)
     idx = np.arange(first_packet, first_packet + n, dtype=np.int64)
-    key_of = (idx % n_keys).astype(np.uint32)
-    pn = (idx // n_keys).astype(np.uint64)
-    # group by key slot (stable), as the host side of the engine does
-    order = np.argsort(key_of, kind="stable")
-    key_of, pn = key_of[order], pn[order]
+    if order == "random":
+        # the global stream's key sequence, sliced for this shard
+        krng = np.random.default_rng(seed + 2)
+        key_of = krng.integers(0, n_keys, first_packet + n).astype(np.uint32)
+        pn = _per_key_counter(key_of, n_keys)[first_packet:]
+        key_of = key_of[first_packet:]
+    else:
+        key_of = (idx % n_keys).astype(np.uint32)
+        pn = (idx // n_keys).astype(np.uint64)
+        if order == "grouped":
+            o = np.argsort(key_of, kind="stable")
+            key_of, pn = key_of[o], pn[o]
+        elif order != "round_robin":
+            raise ValueError(f"unknown order {order!r}")
 
     plain = np.zeros(n * SLOT_BYTES, dtype=np.uint8)
     view = plain.reshape(n, SLOT_BYTES)

@@ -1,7 +1,11 @@
 /*
  * aioquic_amd._crypto -- CPython binding of libquicpp.so (include/quic_pp.h).
  *
- * Object API identical to the reference's aioquic._crypto (src/aioquic/_crypto.pyi:1-15):
+ * Built like the reference's aioquic._crypto: limited API 3.10 (abi3) and
+ * heap types from PyType_FromSpec (src/aioquic/_crypto.c:203-219,358-372,
+ * setup.py:30-39), so one binary serves every CPython >= 3.10.
+ *
+ * Object API identical to the reference (src/aioquic/_crypto.pyi:1-15):
  *   AEAD(cipher_name, key, iv).encrypt(data, associated_data, packet_number) -> bytes
  *                             .decrypt(data, associated_data, packet_number) -> bytes
  *   HeaderProtection(cipher_name, key).apply(plain_header, protected_payload) -> bytes
@@ -10,35 +14,62 @@
  * Every byte of crypto runs on the GPU through libquicpp; there is no CPU path.
  * Without a gfx950 device the constructors raise RuntimeError.
  *
- * Batch API (device pointers as ints, for torch tensors / the batch engine):
- *   KeyTable(capacity) .set(materials) .clear(slots) .capacity
- *   protect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream) -> None
- *   unprotect(...)                                                  -> None
+ * Batch API (pointers are ints: device pointers for the device forms, host
+ * pointers for the *_into forms; the caller keeps the memory alive):
+ *   KeyTable(capacity) .set(materials) .derive(secrets) .clear(slots) .capacity
+ *   Plan(capacity)                                  device scratch of the bucketing step
+ *   protect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream[, plan])   -> None
+ *   unprotect(...)                                                          -> None
+ *   plan_build(plan, table, desc_ptr, n, stream)    bucket a batch by (suite, slot)
  *   protect_host(table, desc, data, out_len) -> (bytes out, bytes results)
  *   unprotect_host(table, desc, data, out_len) -> (bytes out, bytes results)
+ *   protect_into(table, desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr) -> None
+ *   unprotect_into(...)                                                         -> None
  *   hp_mask_host(table, slots, samples) -> bytes
+ *
+ * Threads: host-buffer calls release the GIL.  Each OS thread gets its own
+ * qpp_session (pinned staging + streams; quic_pp.h: a session is single-
+ * threaded), created on first use and destroyed when the thread exits, so
+ * concurrent calls from different threads never share staging.
  */
 #define PY_SSIZE_T_CLEAN
+#define Py_LIMITED_API 0x030A0000
 #include <Python.h>
 #include <ctype.h>
+#include <pthread.h>
 #include <string.h>
 
 #include "quic_pp.h"
 
 static PyObject *g_crypto_error;
-static qpp_session *g_session;
+static PyObject *g_aead_type, *g_hp_type, *g_kt_type, *g_plan_type;
 
+/* ------------------------------------------------------------ sessions -- */
+
+static pthread_key_t g_session_key;
+static pthread_once_t g_session_once = PTHREAD_ONCE_INIT;
+
+static void session_free(void *s) { qpp_session_destroy((qpp_session *)s); }
+static void session_key_init(void) { (void)pthread_key_create(&g_session_key, session_free); }
+
+/* This thread's session, created on first use.  Call with the GIL held. */
 static qpp_session *session(void)
 {
-    if (!g_session) {
-        int rc = qpp_session_create(1 << 16, 64, &g_session);
-        if (rc != QPP_OK) {
-            PyErr_Format(PyExc_RuntimeError, "aioquic_amd: cannot open a gfx950 session (%s)",
-                         qpp_strerror(rc));
-            return NULL;
-        }
+    (void)pthread_once(&g_session_once, session_key_init);
+    qpp_session *s = (qpp_session *)pthread_getspecific(g_session_key);
+    if (s) return s;
+    int rc = qpp_session_create(1 << 16, 64, &s);
+    if (rc != QPP_OK) {
+        PyErr_Format(PyExc_RuntimeError, "aioquic_amd: cannot open a gfx950 session (%s)",
+                     qpp_strerror(rc));
+        return NULL;
     }
-    return g_session;
+    if (pthread_setspecific(g_session_key, s) != 0) {
+        qpp_session_destroy(s);
+        PyErr_SetString(PyExc_RuntimeError, "aioquic_amd: cannot store the thread's session");
+        return NULL;
+    }
+    return s;
 }
 
 static int check_rc(int rc)
@@ -47,6 +78,18 @@ static int check_rc(int rc)
     PyErr_Format(PyExc_RuntimeError, "aioquic_amd: %s", qpp_strerror(rc));
     return -1;
 }
+
+static void *as_ptr(unsigned long long v) { return (void *)(uintptr_t)v; }
+
+static void heap_dealloc(PyObject *self)
+{
+    PyTypeObject *tp = Py_TYPE(self);
+    freefunc f = (freefunc)PyType_GetSlot(tp, Py_tp_free);
+    f(self);
+    Py_DECREF(tp);
+}
+
+/* --------------------------------------------------------- cipher names -- */
 
 static int streq_ci(const char *a, Py_ssize_t alen, const char *b)
 {
@@ -77,7 +120,8 @@ static int suite_key_len(int suite) { return suite == QPP_AES_128_GCM ? 16 : 32;
 
 /* ------------------------------------------------------------ key slot -- */
 
-/* A single-slot device key table, created on first use. */
+/* A single-slot device key table, created on first use.  The slot is
+ * read-only after creation, so objects may be used from any thread. */
 typedef struct {
     qpp_key_material km;
     qpp_keytab *kt;
@@ -86,15 +130,24 @@ typedef struct {
 static int oneslot_ready(OneSlot *o)
 {
     if (o->kt) return 0;
-    if (!session()) return -1;
+    qpp_session *s = session();
+    if (!s) return -1;
     int rc = qpp_keytab_create(1, &o->kt);
-    if (rc == QPP_OK) rc = qpp_session_set_keys(g_session, o->kt, &o->km, 1);
+    if (rc == QPP_OK) rc = qpp_session_set_keys(s, o->kt, &o->km, 1);
     if (rc != QPP_OK) {
         if (o->kt) qpp_keytab_destroy(o->kt);
         o->kt = NULL;
         return check_rc(rc);
     }
     return 0;
+}
+
+static void oneslot_reset(OneSlot *o, int suite)
+{
+    if (o->kt) qpp_keytab_destroy(o->kt);
+    o->kt = NULL;
+    memset(&o->km, 0, sizeof(o->km));
+    o->km.suite = (uint8_t)suite;
 }
 
 /* ---------------------------------------------------------------- AEAD -- */
@@ -129,12 +182,7 @@ static int AEAD_init(AEADObject *self, PyObject *args, PyObject *kwargs)
         PyErr_SetString(g_crypto_error, "OpenSSL call failed");
         return -1;
     }
-    if (self->s.kt) {
-        qpp_keytab_destroy(self->s.kt);
-        self->s.kt = NULL;
-    }
-    memset(&self->s.km, 0, sizeof(self->s.km));
-    self->s.km.suite = (uint8_t)suite;
+    oneslot_reset(&self->s, suite);
     memcpy(self->s.km.key, key, (size_t)key_len);
     memcpy(self->s.km.iv, iv, (size_t)iv_len); /* short iv: zero padded, as the reference */
     return oneslot_ready(&self->s);
@@ -143,7 +191,7 @@ static int AEAD_init(AEADObject *self, PyObject *args, PyObject *kwargs)
 static void AEAD_dealloc(AEADObject *self)
 {
     if (self->s.kt) qpp_keytab_destroy(self->s.kt);
-    Py_TYPE(self)->tp_free((PyObject *)self);
+    heap_dealloc((PyObject *)self);
 }
 
 /* in = aad || data; AEAD only (QPP_F_NO_HP) */
@@ -158,6 +206,8 @@ static PyObject *aead_run(AEADObject *self, PyObject *args, int enc)
         return NULL;
     }
     if (oneslot_ready(&self->s) < 0) return NULL;
+    qpp_session *s = session();
+    if (!s) return NULL;
     size_t in_len = (size_t)(aad_len + data_len);
     size_t out_len = in_len + (enc ? QPP_TAG_LEN : 0);
     unsigned char *buf = PyMem_Malloc(in_len + out_len + 1);
@@ -171,10 +221,8 @@ static PyObject *aead_run(AEADObject *self, PyObject *args, int enc)
     d.flags = QPP_F_NO_HP;
     d.pn = pn;
     qpp_result r;
-    int rc = enc ? qpp_session_protect(g_session, self->s.kt, &d, 1, buf, in_len, buf + in_len,
-                                       out_len, &r)
-                 : qpp_session_unprotect(g_session, self->s.kt, &d, 1, buf, in_len, buf + in_len,
-                                         out_len, &r);
+    int rc = enc ? qpp_session_protect(s, self->s.kt, &d, 1, buf, in_len, buf + in_len, out_len, &r)
+                 : qpp_session_unprotect(s, self->s.kt, &d, 1, buf, in_len, buf + in_len, out_len, &r);
     PyObject *ret = NULL;
     if (check_rc(rc) == 0) {
         if (r.status == QPP_S_OK)
@@ -207,16 +255,17 @@ static PyMethodDef AEAD_methods[] = {
     {NULL},
 };
 
-static PyTypeObject AEADType = {
-    PyVarObject_HEAD_INIT(NULL, 0).tp_name = "aioquic_amd._crypto.AEAD",
-    .tp_basicsize = sizeof(AEADObject),
-    .tp_flags = Py_TPFLAGS_DEFAULT,
-    .tp_doc = "AEAD payload protection on the GPU",
-    .tp_methods = AEAD_methods,
-    .tp_init = (initproc)AEAD_init,
-    .tp_new = PyType_GenericNew,
-    .tp_dealloc = (destructor)AEAD_dealloc,
+static PyType_Slot AEAD_slots[] = {
+    {Py_tp_doc, "AEAD payload protection on the GPU"},
+    {Py_tp_methods, AEAD_methods},
+    {Py_tp_init, AEAD_init},
+    {Py_tp_new, PyType_GenericNew},
+    {Py_tp_dealloc, AEAD_dealloc},
+    {0, NULL},
 };
+
+static PyType_Spec AEAD_spec = {"aioquic_amd._crypto.AEAD", sizeof(AEADObject), 0,
+                                Py_TPFLAGS_DEFAULT, AEAD_slots};
 
 /* ---------------------------------------------------- HeaderProtection -- */
 
@@ -240,28 +289,24 @@ static int HP_init(HPObject *self, PyObject *args, PyObject *kwargs)
         PyErr_SetString(g_crypto_error, "OpenSSL call failed");
         return -1;
     }
-    if (self->s.kt) {
-        qpp_keytab_destroy(self->s.kt);
-        self->s.kt = NULL;
-    }
-    memset(&self->s.km, 0, sizeof(self->s.km));
-    self->s.km.suite = (uint8_t)suite;
+    oneslot_reset(&self->s, suite);
     memcpy(self->s.km.hp, key, (size_t)key_len);
-    /* the AEAD half of the slot is unused by mask launches; give it a valid key */
     return oneslot_ready(&self->s);
 }
 
 static void HP_dealloc(HPObject *self)
 {
     if (self->s.kt) qpp_keytab_destroy(self->s.kt);
-    Py_TYPE(self)->tp_free((PyObject *)self);
+    heap_dealloc((PyObject *)self);
 }
 
 static int hp_mask(HPObject *self, const unsigned char *sample, unsigned char mask[16])
 {
     if (oneslot_ready(&self->s) < 0) return -1;
+    qpp_session *s = session();
+    if (!s) return -1;
     uint32_t slot = 0;
-    return check_rc(qpp_session_hp_mask(g_session, self->s.kt, &slot, sample, 1, mask));
+    return check_rc(qpp_session_hp_mask(s, self->s.kt, &slot, sample, 1, mask));
 }
 
 static unsigned char first_byte_bits(unsigned char b0) { return (b0 & 0x80) ? 0x0f : 0x1f; }
@@ -287,7 +332,7 @@ static PyObject *HP_apply(HPObject *self, PyObject *args)
     if (hp_mask(self, payload + 4 - pn_len, mask) < 0) return NULL;
     PyObject *out = PyBytes_FromStringAndSize(NULL, hlen + plen);
     if (!out) return NULL;
-    unsigned char *o = (unsigned char *)PyBytes_AS_STRING(out);
+    unsigned char *o = (unsigned char *)PyBytes_AsString(out);
     memcpy(o, hdr, (size_t)hlen);
     memcpy(o + hlen, payload, (size_t)plen);
     o[0] ^= mask[0] & first_byte_bits(o[0]);
@@ -336,16 +381,17 @@ static PyMethodDef HP_methods[] = {
     {NULL},
 };
 
-static PyTypeObject HPType = {
-    PyVarObject_HEAD_INIT(NULL, 0).tp_name = "aioquic_amd._crypto.HeaderProtection",
-    .tp_basicsize = sizeof(HPObject),
-    .tp_flags = Py_TPFLAGS_DEFAULT,
-    .tp_doc = "QUIC header protection masks on the GPU",
-    .tp_methods = HP_methods,
-    .tp_init = (initproc)HP_init,
-    .tp_new = PyType_GenericNew,
-    .tp_dealloc = (destructor)HP_dealloc,
+static PyType_Slot HP_slots[] = {
+    {Py_tp_doc, "QUIC header protection masks on the GPU"},
+    {Py_tp_methods, HP_methods},
+    {Py_tp_init, HP_init},
+    {Py_tp_new, PyType_GenericNew},
+    {Py_tp_dealloc, HP_dealloc},
+    {0, NULL},
 };
+
+static PyType_Spec HP_spec = {"aioquic_amd._crypto.HeaderProtection", sizeof(HPObject), 0,
+                              Py_TPFLAGS_DEFAULT, HP_slots};
 
 /* ------------------------------------------------------------ KeyTable -- */
 
@@ -373,26 +419,25 @@ static int KT_init(KeyTableObject *self, PyObject *args, PyObject *kwargs)
 static void KT_dealloc(KeyTableObject *self)
 {
     if (self->kt) qpp_keytab_destroy(self->kt);
-    Py_TYPE(self)->tp_free((PyObject *)self);
+    heap_dealloc((PyObject *)self);
 }
 
 /* set(materials: bytes-like of n packed qpp_key_material records, stream=0) */
 static PyObject *KT_set(KeyTableObject *self, PyObject *args)
 {
-    Py_buffer b;
+    const char *b;
+    Py_ssize_t len;
     unsigned long long stream = 0;
-    if (!PyArg_ParseTuple(args, "y*|K", &b, &stream)) return NULL;
-    if (b.len % (Py_ssize_t)sizeof(qpp_key_material)) {
-        PyBuffer_Release(&b);
+    if (!PyArg_ParseTuple(args, "y#|K", &b, &len, &stream)) return NULL;
+    if (len % (Py_ssize_t)sizeof(qpp_key_material)) {
         PyErr_SetString(PyExc_ValueError, "materials must be a whole number of 84-byte records");
         return NULL;
     }
-    uint32_t n = (uint32_t)(b.len / (Py_ssize_t)sizeof(qpp_key_material));
+    uint32_t n = (uint32_t)(len / (Py_ssize_t)sizeof(qpp_key_material));
     int rc;
     Py_BEGIN_ALLOW_THREADS
-    rc = qpp_keytab_set(self->kt, (const qpp_key_material *)b.buf, n, (void *)(uintptr_t)stream);
+    rc = qpp_keytab_set(self->kt, (const qpp_key_material *)b, n, as_ptr(stream));
     Py_END_ALLOW_THREADS
-    PyBuffer_Release(&b);
     if (rc == QPP_E_ARG) {
         PyErr_SetString(PyExc_ValueError, "bad key material (slot out of range or unknown suite)");
         return NULL;
@@ -405,26 +450,22 @@ static PyObject *KT_set(KeyTableObject *self, PyObject *args)
  * (qpp_keytab_derive); secrets = whole qpp_secret records. */
 static PyObject *KT_derive(KeyTableObject *self, PyObject *args)
 {
-    Py_buffer b;
+    const char *b;
+    Py_ssize_t len;
     unsigned long long stream = 0;
-    if (!PyArg_ParseTuple(args, "y*|K", &b, &stream)) return NULL;
-    if (b.len % (Py_ssize_t)sizeof(qpp_secret)) {
-        PyBuffer_Release(&b);
+    if (!PyArg_ParseTuple(args, "y#|K", &b, &len, &stream)) return NULL;
+    if (len % (Py_ssize_t)sizeof(qpp_secret)) {
         PyErr_SetString(PyExc_ValueError, "secrets must be a whole number of 80-byte records");
         return NULL;
     }
-    uint32_t n = (uint32_t)(b.len / (Py_ssize_t)sizeof(qpp_secret));
+    uint32_t n = (uint32_t)(len / (Py_ssize_t)sizeof(qpp_secret));
     PyObject *km = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_key_material));
-    if (!km) {
-        PyBuffer_Release(&b);
-        return NULL;
-    }
+    if (!km) return NULL;
+    qpp_key_material *out = (qpp_key_material *)PyBytes_AsString(km);
     int rc;
     Py_BEGIN_ALLOW_THREADS
-    rc = qpp_keytab_derive(self->kt, (const qpp_secret *)b.buf, n,
-                           (qpp_key_material *)PyBytes_AS_STRING(km), (void *)(uintptr_t)stream);
+    rc = qpp_keytab_derive(self->kt, (const qpp_secret *)b, n, out, as_ptr(stream));
     Py_END_ALLOW_THREADS
-    PyBuffer_Release(&b);
     if (rc == QPP_E_ARG) {
         Py_DECREF(km);
         PyErr_SetString(PyExc_ValueError, "bad secret (slot out of range, unknown suite or length)");
@@ -439,10 +480,13 @@ static PyObject *KT_derive(KeyTableObject *self, PyObject *args)
 
 static PyObject *KT_clear(KeyTableObject *self, PyObject *args)
 {
-    Py_buffer b;
-    if (!PyArg_ParseTuple(args, "y*", &b)) return NULL;
-    int rc = qpp_keytab_clear(self->kt, (const uint32_t *)b.buf, (uint32_t)(b.len / 4), NULL);
-    PyBuffer_Release(&b);
+    const char *b;
+    Py_ssize_t len;
+    if (!PyArg_ParseTuple(args, "y#", &b, &len)) return NULL;
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = qpp_keytab_clear(self->kt, (const uint32_t *)b, (uint32_t)(len / 4), NULL);
+    Py_END_ALLOW_THREADS
     if (check_rc(rc) < 0) return NULL;
     Py_RETURN_NONE;
 }
@@ -464,41 +508,101 @@ static PyGetSetDef KT_getset[] = {
     {NULL},
 };
 
-static PyTypeObject KTType = {
-    PyVarObject_HEAD_INIT(NULL, 0).tp_name = "aioquic_amd._crypto.KeyTable",
-    .tp_basicsize = sizeof(KeyTableObject),
-    .tp_flags = Py_TPFLAGS_DEFAULT,
-    .tp_doc = "device-resident expanded key slots",
-    .tp_methods = KT_methods,
-    .tp_getset = KT_getset,
-    .tp_init = (initproc)KT_init,
-    .tp_new = PyType_GenericNew,
-    .tp_dealloc = (destructor)KT_dealloc,
+static PyType_Slot KT_slots[] = {
+    {Py_tp_doc, "device-resident expanded key slots"},
+    {Py_tp_methods, KT_methods},
+    {Py_tp_getset, KT_getset},
+    {Py_tp_init, KT_init},
+    {Py_tp_new, PyType_GenericNew},
+    {Py_tp_dealloc, KT_dealloc},
+    {0, NULL},
 };
+
+static PyType_Spec KT_spec = {"aioquic_amd._crypto.KeyTable", sizeof(KeyTableObject), 0,
+                              Py_TPFLAGS_DEFAULT, KT_slots};
 
 static qpp_keytab *as_table(PyObject *o)
 {
-    if (!PyObject_TypeCheck(o, &KTType)) {
+    if (!PyObject_TypeCheck(o, (PyTypeObject *)g_kt_type)) {
         PyErr_SetString(PyExc_TypeError, "expected a KeyTable");
         return NULL;
     }
     return ((KeyTableObject *)o)->kt;
 }
 
+/* ---------------------------------------------------------------- Plan -- */
+
+typedef struct {
+    PyObject_HEAD
+    qpp_plan *plan;
+} PlanObject;
+
+static int Plan_init(PlanObject *self, PyObject *args, PyObject *kwargs)
+{
+    unsigned int cap;
+    if (!PyArg_ParseTuple(args, "I", &cap)) return -1;
+    if (self->plan) {
+        qpp_plan_destroy(self->plan);
+        self->plan = NULL;
+    }
+    int rc = qpp_plan_create(cap, &self->plan);
+    if (rc == QPP_E_ARG) {
+        PyErr_SetString(PyExc_ValueError, "invalid plan capacity");
+        return -1;
+    }
+    return check_rc(rc);
+}
+
+static void Plan_dealloc(PlanObject *self)
+{
+    if (self->plan) qpp_plan_destroy(self->plan);
+    heap_dealloc((PyObject *)self);
+}
+
+static PyType_Slot Plan_slots[] = {
+    {Py_tp_doc, "device scratch of the (suite, key slot) bucketing step"},
+    {Py_tp_init, Plan_init},
+    {Py_tp_new, PyType_GenericNew},
+    {Py_tp_dealloc, Plan_dealloc},
+    {0, NULL},
+};
+
+static PyType_Spec Plan_spec = {"aioquic_amd._crypto.Plan", sizeof(PlanObject), 0,
+                                Py_TPFLAGS_DEFAULT, Plan_slots};
+
+/* NULL for None, else the plan (NULL with an exception set for a wrong type) */
+static int as_plan(PyObject *o, qpp_plan **out)
+{
+    *out = NULL;
+    if (!o || o == Py_None) return 0;
+    if (!PyObject_TypeCheck(o, (PyTypeObject *)g_plan_type)) {
+        PyErr_SetString(PyExc_TypeError, "expected a Plan or None");
+        return -1;
+    }
+    *out = ((PlanObject *)o)->plan;
+    return 0;
+}
+
 /* -------------------------------------------------------- batch calls -- */
 
+/* protect / unprotect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream[, plan]) */
 static PyObject *batch_dev(PyObject *args, int enc)
 {
-    PyObject *t;
+    PyObject *t, *po = NULL;
     unsigned long long dp, ip, op, rp, sp;
     unsigned int n;
-    if (!PyArg_ParseTuple(args, "OKIKKKK", &t, &dp, &n, &ip, &op, &rp, &sp)) return NULL;
+    if (!PyArg_ParseTuple(args, "OKIKKKK|O", &t, &dp, &n, &ip, &op, &rp, &sp, &po)) return NULL;
     qpp_keytab *kt = as_table(t);
-    if (!kt) return NULL;
-    int rc = enc ? qpp_protect(kt, (const qpp_desc *)(uintptr_t)dp, n, (const uint8_t *)(uintptr_t)ip,
-                               (uint8_t *)(uintptr_t)op, (qpp_result *)(uintptr_t)rp, (void *)(uintptr_t)sp)
-                 : qpp_unprotect(kt, (const qpp_desc *)(uintptr_t)dp, n, (const uint8_t *)(uintptr_t)ip,
-                                 (uint8_t *)(uintptr_t)op, (qpp_result *)(uintptr_t)rp, (void *)(uintptr_t)sp);
+    qpp_plan *plan;
+    if (!kt || as_plan(po, &plan) < 0) return NULL;
+    int rc = plan ? (enc ? qpp_protect_planned : qpp_unprotect_planned)(
+                        kt, plan, as_ptr(dp), n, as_ptr(ip), as_ptr(op), as_ptr(rp), as_ptr(sp))
+                  : (enc ? qpp_protect : qpp_unprotect)(kt, as_ptr(dp), n, as_ptr(ip), as_ptr(op),
+                                                        as_ptr(rp), as_ptr(sp));
+    if (rc == QPP_E_ARG) {
+        PyErr_SetString(PyExc_ValueError, "bad batch arguments (n beyond the plan's capacity?)");
+        return NULL;
+    }
     if (check_rc(rc) < 0) return NULL;
     Py_RETURN_NONE;
 }
@@ -506,111 +610,131 @@ static PyObject *batch_dev(PyObject *args, int enc)
 static PyObject *py_protect(PyObject *m, PyObject *args) { return batch_dev(args, 1); }
 static PyObject *py_unprotect(PyObject *m, PyObject *args) { return batch_dev(args, 0); }
 
+/* plan_build(plan, table, desc_ptr, n, stream) */
+static PyObject *py_plan_build(PyObject *m, PyObject *args)
+{
+    PyObject *po, *t;
+    unsigned long long dp, sp;
+    unsigned int n;
+    if (!PyArg_ParseTuple(args, "OOKIK", &po, &t, &dp, &n, &sp)) return NULL;
+    qpp_keytab *kt = as_table(t);
+    qpp_plan *plan;
+    if (!kt || as_plan(po, &plan) < 0) return NULL;
+    if (!plan) {
+        PyErr_SetString(PyExc_TypeError, "expected a Plan");
+        return NULL;
+    }
+    int rc = qpp_plan_build(plan, kt, as_ptr(dp), n, as_ptr(sp));
+    if (rc == QPP_E_ARG) {
+        PyErr_SetString(PyExc_ValueError, "batch larger than the plan's capacity");
+        return NULL;
+    }
+    if (check_rc(rc) < 0) return NULL;
+    Py_RETURN_NONE;
+}
+
+static int host_call(int enc, qpp_keytab *kt, const void *desc, uint32_t n, const void *in,
+                     size_t in_len, void *out, size_t out_len, void *res)
+{
+    qpp_session *s = session();
+    if (!s) return -1;
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = enc ? qpp_session_protect(s, kt, desc, n, in, in_len, out, out_len, res)
+             : qpp_session_unprotect(s, kt, desc, n, in, in_len, out, out_len, res);
+    Py_END_ALLOW_THREADS
+    return check_rc(rc);
+}
+
+/* protect_host / unprotect_host(table, desc, data, out_len) -> (out, results) */
 static PyObject *batch_host(PyObject *args, int enc)
 {
     PyObject *t;
-    Py_buffer desc, data;
-    Py_ssize_t out_len;
-    if (!PyArg_ParseTuple(args, "Oy*y*n", &t, &desc, &data, &out_len)) return NULL;
-    PyObject *ret = NULL, *out = NULL, *res = NULL;
+    const char *desc, *data;
+    Py_ssize_t desc_len, data_len, out_len;
+    if (!PyArg_ParseTuple(args, "Oy#y#n", &t, &desc, &desc_len, &data, &data_len, &out_len))
+        return NULL;
     qpp_keytab *kt = as_table(t);
-    if (!kt || !session()) goto done;
-    if (desc.len % (Py_ssize_t)sizeof(qpp_desc) || out_len < 0) {
+    if (!kt) return NULL;
+    if (desc_len % (Py_ssize_t)sizeof(qpp_desc) || out_len < 0) {
         PyErr_SetString(PyExc_ValueError, "bad descriptor buffer or output length");
-        goto done;
+        return NULL;
     }
-    uint32_t n = (uint32_t)(desc.len / (Py_ssize_t)sizeof(qpp_desc));
-    out = PyBytes_FromStringAndSize(NULL, out_len);
-    res = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_result));
-    if (!out || !res) goto done;
-    /* the session writes every byte of out (zeros where no packet lands) for
-       n > 0, so only an empty batch needs the zero fill here */
-    if (n == 0) memset(PyBytes_AS_STRING(out), 0, (size_t)out_len);
-    int rc;
-    Py_BEGIN_ALLOW_THREADS
-    rc = enc ? qpp_session_protect(g_session, kt, desc.buf, n, data.buf, (size_t)data.len,
-                                   (uint8_t *)PyBytes_AS_STRING(out), (size_t)out_len,
-                                   (qpp_result *)PyBytes_AS_STRING(res))
-             : qpp_session_unprotect(g_session, kt, desc.buf, n, data.buf, (size_t)data.len,
-                                     (uint8_t *)PyBytes_AS_STRING(out), (size_t)out_len,
-                                     (qpp_result *)PyBytes_AS_STRING(res));
-    Py_END_ALLOW_THREADS
-    if (check_rc(rc) < 0) goto done;
-    ret = PyTuple_Pack(2, out, res);
-done:
+    uint32_t n = (uint32_t)(desc_len / (Py_ssize_t)sizeof(qpp_desc));
+    PyObject *out = PyBytes_FromStringAndSize(NULL, out_len);
+    PyObject *res = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_result));
+    PyObject *ret = NULL;
+    if (out && res) {
+        char *o = PyBytes_AsString(out);
+        /* the session writes every byte of out (zeros where no packet lands)
+           for n > 0, so only an empty batch needs the zero fill here */
+        if (n == 0) memset(o, 0, (size_t)out_len);
+        if (host_call(enc, kt, desc, n, data, (size_t)data_len, o, (size_t)out_len,
+                      PyBytes_AsString(res)) == 0)
+            ret = PyTuple_Pack(2, out, res);
+    }
     Py_XDECREF(out);
     Py_XDECREF(res);
-    PyBuffer_Release(&desc);
-    PyBuffer_Release(&data);
     return ret;
 }
 
-/* protect_into / unprotect_into(table, desc, data, out, results): the host
-   form with caller-owned, writable output and result buffers (any buffer
-   object, e.g. a numpy array reused across batches), so a large batch does
-   not allocate and first-touch a fresh bytes object per call. */
+static PyObject *py_protect_host(PyObject *m, PyObject *args) { return batch_host(args, 1); }
+static PyObject *py_unprotect_host(PyObject *m, PyObject *args) { return batch_host(args, 0); }
+
+/* protect_into / unprotect_into(table, desc_ptr, n, in_ptr, in_len, out_ptr,
+   out_len, res_ptr): host memory given by address (e.g. numpy arrays reused
+   across batches), so a large batch neither allocates nor first-touches a
+   fresh bytes object per call.  The caller keeps the memory alive. */
 static PyObject *batch_into(PyObject *args, int enc)
 {
     PyObject *t;
-    Py_buffer desc, data, out, res;
-    if (!PyArg_ParseTuple(args, "Oy*y*w*w*", &t, &desc, &data, &out, &res)) return NULL;
-    PyObject *ret = NULL;
+    unsigned long long dp, ip, op, rp, in_len, out_len;
+    unsigned int n;
+    if (!PyArg_ParseTuple(args, "OKIKKKKK", &t, &dp, &n, &ip, &in_len, &op, &out_len, &rp))
+        return NULL;
     qpp_keytab *kt = as_table(t);
-    if (!kt || !session()) goto done;
-    if (desc.len % (Py_ssize_t)sizeof(qpp_desc)) {
-        PyErr_SetString(PyExc_ValueError, "bad descriptor buffer");
-        goto done;
+    if (!kt) return NULL;
+    if (n == 0) {
+        if (out_len) memset(as_ptr(op), 0, (size_t)out_len);
+        Py_RETURN_NONE;
     }
-    uint32_t n = (uint32_t)(desc.len / (Py_ssize_t)sizeof(qpp_desc));
-    if (res.len < (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_result)) {
-        PyErr_SetString(PyExc_ValueError, "results buffer too small");
-        goto done;
+    if (!dp || !rp || (in_len && !ip) || (out_len && !op)) {
+        PyErr_SetString(PyExc_ValueError, "null buffer");
+        return NULL;
     }
-    if (n == 0) memset(out.buf, 0, (size_t)out.len);
-    int rc;
-    Py_BEGIN_ALLOW_THREADS
-    rc = enc ? qpp_session_protect(g_session, kt, desc.buf, n, data.buf, (size_t)data.len,
-                                   (uint8_t *)out.buf, (size_t)out.len, (qpp_result *)res.buf)
-             : qpp_session_unprotect(g_session, kt, desc.buf, n, data.buf, (size_t)data.len,
-                                     (uint8_t *)out.buf, (size_t)out.len, (qpp_result *)res.buf);
-    Py_END_ALLOW_THREADS
-    if (check_rc(rc) < 0) goto done;
-    ret = Py_None;
-    Py_INCREF(ret);
-done:
-    PyBuffer_Release(&desc);
-    PyBuffer_Release(&data);
-    PyBuffer_Release(&out);
-    PyBuffer_Release(&res);
-    return ret;
+    if (host_call(enc, kt, as_ptr(dp), n, as_ptr(ip), (size_t)in_len, as_ptr(op), (size_t)out_len,
+                  as_ptr(rp)) < 0)
+        return NULL;
+    Py_RETURN_NONE;
 }
 
 static PyObject *py_protect_into(PyObject *m, PyObject *args) { return batch_into(args, 1); }
 static PyObject *py_unprotect_into(PyObject *m, PyObject *args) { return batch_into(args, 0); }
 
-static PyObject *py_protect_host(PyObject *m, PyObject *args) { return batch_host(args, 1); }
-static PyObject *py_unprotect_host(PyObject *m, PyObject *args) { return batch_host(args, 0); }
-
 static PyObject *py_hp_mask_host(PyObject *m, PyObject *args)
 {
     PyObject *t;
-    Py_buffer slots, samples;
-    if (!PyArg_ParseTuple(args, "Oy*y*", &t, &slots, &samples)) return NULL;
-    PyObject *out = NULL;
+    const char *slots, *samples;
+    Py_ssize_t slots_len, samples_len;
+    if (!PyArg_ParseTuple(args, "Oy#y#", &t, &slots, &slots_len, &samples, &samples_len))
+        return NULL;
     qpp_keytab *kt = as_table(t);
-    uint32_t n = (uint32_t)(slots.len / 4);
-    if (kt && session()) {
-        if (samples.len != (Py_ssize_t)n * 16) {
-            PyErr_SetString(PyExc_ValueError, "need 16 sample bytes per slot");
-        } else {
-            out = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * 16);
-            if (out && check_rc(qpp_session_hp_mask(g_session, kt, slots.buf, samples.buf, n,
-                                                    (uint8_t *)PyBytes_AS_STRING(out))) < 0)
-                Py_CLEAR(out);
-        }
+    if (!kt) return NULL;
+    uint32_t n = (uint32_t)(slots_len / 4);
+    if (samples_len != (Py_ssize_t)n * 16) {
+        PyErr_SetString(PyExc_ValueError, "need 16 sample bytes per slot");
+        return NULL;
     }
-    PyBuffer_Release(&slots);
-    PyBuffer_Release(&samples);
+    qpp_session *s = session();
+    if (!s) return NULL;
+    PyObject *out = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * 16);
+    if (!out) return NULL;
+    uint8_t *o = (uint8_t *)PyBytes_AsString(out);
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = qpp_session_hp_mask(s, kt, (const uint32_t *)slots, (const uint8_t *)samples, n, o);
+    Py_END_ALLOW_THREADS
+    if (check_rc(rc) < 0) Py_CLEAR(out);
     return out;
 }
 
@@ -625,12 +749,13 @@ static PyObject *py_abi(PyObject *m, PyObject *unused)
 }
 
 static PyMethodDef module_methods[] = {
-    {"protect", py_protect, METH_VARARGS, "protect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream)"},
-    {"unprotect", py_unprotect, METH_VARARGS, "unprotect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream)"},
+    {"protect", py_protect, METH_VARARGS, "protect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream, plan=None)"},
+    {"unprotect", py_unprotect, METH_VARARGS, "unprotect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream, plan=None)"},
+    {"plan_build", py_plan_build, METH_VARARGS, "plan_build(plan, table, desc_ptr, n, stream)"},
     {"protect_host", py_protect_host, METH_VARARGS, "protect_host(table, desc, data, out_len) -> (out, results)"},
     {"unprotect_host", py_unprotect_host, METH_VARARGS, "unprotect_host(table, desc, data, out_len) -> (out, results)"},
-    {"protect_into", py_protect_into, METH_VARARGS, "protect_into(table, desc, data, out, results) -> None"},
-    {"unprotect_into", py_unprotect_into, METH_VARARGS, "unprotect_into(table, desc, data, out, results) -> None"},
+    {"protect_into", py_protect_into, METH_VARARGS, "protect_into(table, desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
+    {"unprotect_into", py_unprotect_into, METH_VARARGS, "unprotect_into(table, desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},
@@ -642,20 +767,28 @@ static struct PyModuleDef moduledef = {
     -1, module_methods,
 };
 
+static int add_type(PyObject *m, PyType_Spec *spec, const char *name, PyObject **slot)
+{
+    PyObject *t = PyType_FromSpec(spec);
+    if (!t) return -1;
+    *slot = t;
+    Py_INCREF(t);
+    return PyModule_AddObject(m, name, t);
+}
+
 PyMODINIT_FUNC PyInit__crypto(void)
 {
     PyObject *m = PyModule_Create(&moduledef);
     if (!m) return NULL;
     g_crypto_error = PyErr_NewException("aioquic_amd._crypto.CryptoError", PyExc_ValueError, NULL);
-    if (!g_crypto_error || PyModule_AddObject(m, "CryptoError", g_crypto_error) < 0) return NULL;
+    if (!g_crypto_error) return NULL;
     Py_INCREF(g_crypto_error);
-    PyTypeObject *types[] = {&AEADType, &HPType, &KTType};
-    const char *names[] = {"AEAD", "HeaderProtection", "KeyTable"};
-    for (int i = 0; i < 3; ++i) {
-        if (PyType_Ready(types[i]) < 0) return NULL;
-        Py_INCREF(types[i]);
-        if (PyModule_AddObject(m, names[i], (PyObject *)types[i]) < 0) return NULL;
-    }
+    if (PyModule_AddObject(m, "CryptoError", g_crypto_error) < 0) return NULL;
+    if (add_type(m, &AEAD_spec, "AEAD", &g_aead_type) < 0 ||
+        add_type(m, &HP_spec, "HeaderProtection", &g_hp_type) < 0 ||
+        add_type(m, &KT_spec, "KeyTable", &g_kt_type) < 0 ||
+        add_type(m, &Plan_spec, "Plan", &g_plan_type) < 0)
+        return NULL;
     PyModule_AddIntConstant(m, "DESC_SIZE", (long)sizeof(qpp_desc));
     PyModule_AddIntConstant(m, "RESULT_SIZE", (long)sizeof(qpp_result));
     PyModule_AddIntConstant(m, "KEY_MATERIAL_SIZE", (long)sizeof(qpp_key_material));

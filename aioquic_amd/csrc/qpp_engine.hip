@@ -23,6 +23,7 @@
 #include "qpp_chacha.h"
 #include "qpp_device.h"
 #include "qpp_hkdf.h"
+#include "qpp_internal.h"
 
 namespace qpp {
 
@@ -41,6 +42,10 @@ constexpr int kScratch = 112;
 constexpr int kScrTail = 32, kScrEj0 = 48, kScrPark = 64, kScrHdr = 96;
 constexpr int kStageBytes = 64 * 16;  // one 16-byte block per lane of a wave
 constexpr uint32_t kNoSlot = 0xffffffffu;
+// Descriptor flag set by the host session for a descriptor whose extents do
+// not fit the caller's buffers: the packet reports QPP_S_LENGTH and no byte
+// of it is read or written.
+constexpr uint32_t kFlagReject = 0x8000u;
 #ifndef QPP_BALANCE
 #define QPP_BALANCE 1
 #endif
@@ -226,7 +231,7 @@ template <bool ENC>
 __device__ __forceinline__ HdrPre prefetch_hdr(const qpp_desc &d, const uint8_t *gin, bool valid)
 {
     HdrPre r = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, 0};
-    if (!valid) return r;
+    if (!valid || (d.flags & kFlagReject)) return r;
     const uint8_t *src = gin + d.in_off;
     const bool hp = !(d.flags & QPP_F_NO_HP) && d.hdr_len >= 1;
     const uint64_t region = ENC ? (uint64_t)d.hdr_len + d.len : (uint64_t)d.len;
@@ -259,7 +264,9 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const HdrPre &pre, c
     P.fbm = 0;
     P.hlen = 0;
     P.clen = 0;
-    if (ENC) {
+    if (d.flags & kFlagReject) {
+        P.status = QPP_S_LENGTH;
+    } else if (ENC) {
         P.hlen = d.hdr_len;
         P.clen = (int)d.len;
         if (P.clen > QPP_PACKET_MAX || P.hlen > QPP_MAX_HDR) P.status = QPP_S_LENGTH;
@@ -352,6 +359,19 @@ __device__ __forceinline__ void write_header(const Pkt &P, int sub, bool masked,
         if (masked) h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
         st_part(P.dst + 16 * q, h, nb);
     }
+}
+
+// A packet whose tag does not verify leaves no plaintext behind: its quad
+// overwrites the payload it streamed out with zeros (quic_pp.h, Authentication
+// failures).  Runs only on the failure path.  Each 16-byte block is cleared
+// by the lane that wrote it (own(i) = that lane), so the zeros land after the
+// plaintext in that lane's program order.
+template <class OWN>
+__device__ __forceinline__ void wipe_payload(const Pkt &P, int sub, OWN own)
+{
+    uint8_t *o = P.dst + P.hlen;
+    for (int i = 0; 16 * i < P.clen; ++i)
+        if (own(i) == sub) st_part(o + 16 * i, u32x4{0, 0, 0, 0}, min(16, P.clen - 16 * i));
 }
 
 // 128-bit little-endian shift right by s bytes (0..15)
@@ -632,7 +652,11 @@ __device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, u
         else write_header(P, sub, false, h0);
     } else {
         const u32x4 diff = got_tag ^ tag;
-        if ((diff.x | diff.y | diff.z | diff.w) != 0) P.status = QPP_S_DECRYPT;
+        if ((diff.x | diff.y | diff.z | diff.w) != 0) {
+            P.status = QPP_S_DECRYPT;
+            // CT block i sits at sequence position pad + za + i (gcm_packet)
+            wipe_payload(P, sub, [&](int i) { return (pad + za + i) & 3; });
+        }
         write_header(P, sub, P.hp, h0);
     }
 }
@@ -797,14 +821,18 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     } else {
         const u32x4 got = ld16(pin + P.clen);
         const u32x4 diff = got ^ tag;
-        if ((diff.x | diff.y | diff.z | diff.w) != 0) P.status = QPP_S_DECRYPT;
+        if ((diff.x | diff.y | diff.z | diff.w) != 0) {
+            P.status = QPP_S_DECRYPT;
+            // chunk c (blocks 4c..4c+3) is unit c (c < 3) or c + 1 of the quad
+            wipe_payload(P, sub, [&](int i) { const int c = i >> 2; return c < 3 ? c : (c + 1) & 3; });
+        }
     }
 }
 
 template <bool ENC>
 __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int sub, const Pkt &P)
 {
-    if (sub != 0) return;
+    if (sub != 0) return;  // p: the packet's index in the caller's order
     const uint32_t out_len =
         P.status == QPP_S_OK ? (uint32_t)(P.hlen + P.clen + (ENC ? QPP_TAG_LEN : 0)) : 0u;
     res[p] = qpp_result{P.pn, (uint16_t)P.status, (uint16_t)P.hlen, out_len};
@@ -826,11 +854,20 @@ __global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WP
                                                 const uint8_t *__restrict__ gtab, uint32_t cap,
                                                 const qpp_desc *__restrict__ desc, uint32_t n,
                                                 const uint8_t *gin, uint8_t *gout,
-                                                qpp_result *__restrict__ res)
+                                                qpp_result *__restrict__ res,
+                                                const uint32_t *__restrict__ range)
 {
     constexpr bool kGcm = SUITE != QPP_CHACHA20_POLY1305;
     constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
     constexpr int kPktPerWG = WG / 4;
+    // Planned launch (range != null): desc is the plan's bucket-ordered copy,
+    // this suite's packets are positions [range[2 SUITE], range[2 SUITE + 1]),
+    // and a packet's result goes to res[desc.rsv] (its index in the caller's
+    // order).  Otherwise positions [0, n) and res[position].
+    const uint32_t base = range ? range[2 * SUITE] : 0u;
+    const uint32_t lim = range ? range[2 * SUITE + 1] : n;
+    if (base + blockIdx.x * kPktPerWG >= lim) return;  // past this suite's bucket
+    auto res_of = [&](uint32_t p, const qpp_desc &dd) -> uint32_t { return range ? dd.rsv : p; };
     __shared__ SuiteSmem<SUITE, WG> sm;
     // Thread-derived values are recomputed where they are used, from the
     // wave index (an SGPR) and a fresh lane id, instead of being kept live
@@ -838,7 +875,7 @@ __global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WP
     // loop is spilled to scratch (HBM traffic and latency).
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     auto tid_now = [&]() -> uint32_t { return (wv << 6) | lane_fresh(); };
-    auto pkt_of = [&](uint32_t t) -> uint32_t { return blockIdx.x * kPktPerWG + (t >> 2); };
+    auto pkt_of = [&](uint32_t t) -> uint32_t { return base + blockIdx.x * kPktPerWG + (t >> 2); };
     QPP_PROBE_AT(0);
 
     // Prologue: everything that depends only on the descriptor is requested
@@ -849,7 +886,7 @@ __global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WP
     uint64_t in0 = ~0ull, out0 = ~0ull;
     {
         const uint32_t p = pkt_of(threadIdx.x);
-        const bool valid = p < n;
+        const bool valid = p < lim;
         qpp_desc d = {};
         if (valid) d = desc[p];
 #ifdef QPP_PROBE
@@ -870,7 +907,7 @@ __global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WP
     // its first packet (host batches are grouped by slot) and stage it now
     uint32_t staged = kNoSlot;
     if constexpr (kGcm) {
-        const uint32_t spec = __builtin_amdgcn_readfirstlane(desc[blockIdx.x * kPktPerWG].slot);
+        const uint32_t spec = __builtin_amdgcn_readfirstlane(desc[base + blockIdx.x * kPktPerWG].slot);
         if (spec < cap) {
             stage_key<WG>(sm, slots, gtab, spec);
             staged = spec;
@@ -923,14 +960,14 @@ __global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WP
         QPP_PROBE_AT(1);
         // the descriptor is re-read each iteration (an L2 hit after the prologue)
         const uint32_t t1 = tid_now(), p1 = pkt_of(t1);
-        const qpp_desc d = p1 < n ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
+        const qpp_desc d = p1 < lim ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
         const bool in_slot = d.slot == cur;
         {
             const uint32_t m = wave_min_u32(d.slot > cur ? d.slot : kNoSlot);
             if (__lane_id() == 0 && m != kNoSlot) atomicMin(&sm.cur_slot[(it + 1) & 1], m);
         }
         if (in_slot && suite > QPP_CHACHA20_POLY1305 && (t1 & 3) == 0)
-            res[p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
+            res[res_of(p1, d)] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
         if (in_slot && mine) {
             const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
             if constexpr (kGcm) {
@@ -975,14 +1012,14 @@ __global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WP
                         P.status = QPP_S_LENGTH;  // workgroup spans more than 4 GiB
                     }
                 }
-                const uint32_t t3 = tid_now();
-                write_result<ENC>(res, pkt_of(t3), t3 & 3, P);
+                const uint32_t t3 = tid_now(), p3 = pkt_of(t3);
+                write_result<ENC>(res, range ? desc[p3].rsv : p3, t3 & 3, P);
                 QPP_PROBE_AT(5);
             } else {
                 const ConstTe T;
                 Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
                 if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, t1 & 3, sm.scratch[t1 >> 2]);
-                write_result<ENC>(res, p1, t1 & 3, P);
+                write_result<ENC>(res, res_of(p1, d), t1 & 3, P);
             }
         }
         __syncthreads();
@@ -1164,8 +1201,27 @@ struct qpp_keytab {
     uint8_t *d_gtab;
     qpp_key_material *d_km;
     uint32_t km_cap;
-    uint32_t suite_mask;  // bit s set once a slot of suite s was installed
+    uint8_t *h_suite;      // host mirror: suite of every slot (0xff = empty)
+    uint32_t n_suite[3];   // installed slots per suite
 };
+
+// Host mirror of the slots' suites, so a launch goes only to the suites the
+// table holds right now (set, derive and clear keep it current).
+static void keytab_note(qpp_keytab *kt, uint32_t slot, uint32_t suite)
+{
+    const uint8_t old = kt->h_suite[slot];
+    if (old <= QPP_CHACHA20_POLY1305) --kt->n_suite[old];
+    kt->h_suite[slot] = (uint8_t)suite;
+    if (suite <= QPP_CHACHA20_POLY1305) ++kt->n_suite[suite];
+}
+
+static uint32_t keytab_suite_mask(const qpp_keytab *kt)
+{
+    uint32_t m = 0;
+    for (int s = 0; s < 3; ++s)
+        if (kt->n_suite[s]) m |= 1u << s;
+    return m;
+}
 
 // Host batches of at least 2 x kPipeChunkBytes of output go through the
 // session as a three-stage pipeline of up to kPipeMaxChunks chunks (see
@@ -1183,7 +1239,12 @@ struct qpp_session {
     uint8_t *h_in, *h_out, *h_misc;  // pinned
     uint8_t *d_in, *d_out, *d_misc;
     size_t misc_bytes;
+    qpp_plan *plan;                  // bucketing of batches of >= kSessionPlanMin packets
 };
+
+// Host batches of at least this many packets are bucketed by (suite, slot)
+// on the device before launch (qpp_plan); smaller ones launch as given.
+constexpr uint32_t kSessionPlanMin = 128;
 
 #define HIPCHK(x)                          \
     do {                                   \
@@ -1232,6 +1293,12 @@ int qpp_keytab_create(uint32_t capacity, qpp_keytab **out)
     if (!kt) return QPP_E_NOMEM;
     kt->cap = capacity;
     (void)hipGetDevice(&kt->device);
+    kt->h_suite = (uint8_t *)malloc(capacity);
+    if (!kt->h_suite) {
+        free(kt);
+        return QPP_E_NOMEM;
+    }
+    memset(kt->h_suite, 0xff, capacity);
     if (hipMalloc(&kt->d_slots, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
         hipMalloc(&kt->d_gtab, (size_t)capacity * kGhashTabBytes) != hipSuccess ||
         hipMemset(kt->d_slots, 0xff, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
@@ -1250,6 +1317,7 @@ void qpp_keytab_destroy(qpp_keytab *kt)
     if (kt->d_slots) (void)hipFree(kt->d_slots);
     if (kt->d_gtab) (void)hipFree(kt->d_gtab);
     if (kt->d_km) (void)hipFree(kt->d_km);
+    free(kt->h_suite);
     free(kt);
 }
 
@@ -1261,7 +1329,7 @@ int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void 
     if (n == 0) return QPP_OK;
     for (uint32_t i = 0; i < n; ++i)
         if (km[i].slot >= kt->cap || km[i].suite > QPP_CHACHA20_POLY1305) return QPP_E_ARG;
-    for (uint32_t i = 0; i < n; ++i) kt->suite_mask |= 1u << km[i].suite;
+    for (uint32_t i = 0; i < n; ++i) keytab_note(kt, km[i].slot, km[i].suite);
     hipStream_t s = (hipStream_t)stream;
     if (n > kt->km_cap) {
         if (kt->d_km) HIPCHK(hipFree(kt->d_km));
@@ -1289,7 +1357,7 @@ int qpp_keytab_derive(qpp_keytab *kt, const qpp_secret *sec, uint32_t n,
         if (sec[i].slot >= kt->cap || sec[i].suite > QPP_CHACHA20_POLY1305 ||
             sec[i].secret_len < 1 || sec[i].secret_len > 64)
             return QPP_E_ARG;
-    for (uint32_t i = 0; i < n; ++i) kt->suite_mask |= 1u << sec[i].suite;
+    for (uint32_t i = 0; i < n; ++i) keytab_note(kt, sec[i].slot, sec[i].suite);
     hipStream_t s = (hipStream_t)stream;
     if (n > kt->km_cap) {
         if (kt->d_km) HIPCHK(hipFree(kt->d_km));
@@ -1325,6 +1393,8 @@ int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *st
 {
     if (!kt || (!slots && n)) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (slots[i] < kt->cap) keytab_note(kt, slots[i], 0xffu);
     hipStream_t s = (hipStream_t)stream;
     uint32_t *d = NULL;
     HIPCHK(hipMalloc(&d, (size_t)n * 4));
@@ -1356,14 +1426,17 @@ static int wg_choice(const char *env, int dflt, bool chacha)
 }
 
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
-                          const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream)
+                          const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream,
+                          const uint32_t *d_range = nullptr)
 {
     if (!kt || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
     hipStream_t s = (hipStream_t)stream;
-    // one launch per suite installed in the table (an empty table still
-    // gets one launch so every packet reports QPP_S_NO_KEY)
-    const uint32_t mask = kt->suite_mask ? kt->suite_mask : 1u;
+    // one launch per suite the table holds now; unplanned, an empty table
+    // still gets one launch so every packet reports QPP_S_NO_KEY (planned,
+    // the no-key bucket has its own kernel)
+    uint32_t mask = keytab_suite_mask(kt);
+    if (!mask && !d_range) mask = 1u;
     const int wg_gcm = wg_choice("QPP_WG_GCM", kGcmWG, false);
     const int wg_cc = enc ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
                           : wg_choice("QPP_WG_CHACHA_DEC", kChachaWGDec, true);
@@ -1372,10 +1445,10 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
         const dim3 grid((n + WGV / 4 - 1) / (WGV / 4)), block(WGV);                            \
         if (enc)                                                                               \
             hipLaunchKernelGGL((k_packets<SUITE, true, WGV>), grid, block, 0, s, kt->d_slots,  \
-                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);            \
+                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_range);   \
         else                                                                                   \
             hipLaunchKernelGGL((k_packets<SUITE, false, WGV>), grid, block, 0, s, kt->d_slots, \
-                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);            \
+                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_range);   \
     } while (0)
 #define QPP_LAUNCH_GCM(SUITE)                                                                  \
     if (mask & (1u << SUITE)) {                                                                \
@@ -1407,6 +1480,40 @@ int qpp_unprotect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                   const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream)
 {
     return launch_packets(false, kt, d_desc, n, d_in, d_out, d_res, stream);
+}
+
+int qpp_plan_build(qpp_plan *p, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
+                   void *stream)
+{
+    if (!p || !kt || (n && !d_desc)) return QPP_E_ARG;
+    return qpp_internal_plan_build(p, kt->d_slots, kt->cap, d_desc, n, (hipStream_t)stream);
+}
+
+static int launch_planned(bool enc, const qpp_keytab *kt, const qpp_plan *p, const qpp_desc *d_desc,
+                          uint32_t n, const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res,
+                          void *stream)
+{
+    if (!kt || !p || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = qpp_internal_plan_gather(p, d_desc, n, s);
+    if (rc == QPP_OK)
+        rc = launch_packets(enc, kt, p->d_sorted, n, d_in, d_out, d_res, stream, p->d_range);
+    if (rc == QPP_OK) rc = qpp_internal_plan_nokey(p, d_res, s);
+    return rc;
+}
+
+int qpp_protect_planned(const qpp_keytab *kt, const qpp_plan *p, const qpp_desc *d_desc, uint32_t n,
+                        const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream)
+{
+    return launch_planned(true, kt, p, d_desc, n, d_in, d_out, d_res, stream);
+}
+
+int qpp_unprotect_planned(const qpp_keytab *kt, const qpp_plan *p, const qpp_desc *d_desc,
+                          uint32_t n, const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res,
+                          void *stream)
+{
+    return launch_planned(false, kt, p, d_desc, n, d_in, d_out, d_res, stream);
 }
 
 int qpp_hp_mask(const qpp_keytab *kt, const uint32_t *d_slots, const uint8_t *d_samples,
@@ -1505,6 +1612,7 @@ void qpp_session_destroy(qpp_session *s)
     if (s->s_in) (void)hipStreamSynchronize(s->s_in);
     if (s->s_out) (void)hipStreamSynchronize(s->s_out);
     session_free_buffers(s);
+    qpp_plan_destroy(s->plan);
     for (int c = 0; c < kPipeMaxChunks; ++c) {
         if (s->ev_in[c]) (void)hipEventDestroy(s->ev_in[c]);
         if (s->ev_k[c]) (void)hipEventDestroy(s->ev_k[c]);
@@ -1560,6 +1668,42 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
         if (th[t].joinable()) th[t].join();
 }
 
+// Descriptor extents against the caller's buffer sizes (quic_pp.h, Buffers):
+// a descriptor that does not fit is flagged so the kernel reports
+// QPP_S_LENGTH for it without touching memory.  Protect reads header +
+// payload and writes header + ciphertext + tag; unprotect reads and writes
+// at most the packet's length.
+static void reject_out_of_bounds(bool enc, qpp_desc *d, uint32_t n, size_t in_len, size_t out_len)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t rd = enc ? (uint64_t)d[i].hdr_len + d[i].len : (uint64_t)d[i].len;
+        const uint64_t wr = enc ? rd + QPP_TAG_LEN : rd;
+        const bool ok = d[i].in_off <= in_len && rd <= in_len - d[i].in_off && d[i].out_off <= out_len &&
+                        wr <= out_len - d[i].out_off;
+        d[i].flags = ok ? (uint16_t)(d[i].flags & ~kFlagReject) : (uint16_t)(d[i].flags | kFlagReject);
+    }
+}
+
+// One launch over n device descriptors of the session: bucketed by (suite,
+// slot) through the session's plan when the batch is large enough.
+static int session_launch(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp_desc *dd,
+                          uint32_t n, qpp_result *dr)
+{
+    if (n < kSessionPlanMin) return launch_packets(enc, kt, dd, n, s->d_in, s->d_out, dr, s->stream);
+    if (s->plan && s->plan->cap < n) {
+        HIPCHK(hipStreamSynchronize(s->stream));  // the old plan may still be in use
+        qpp_plan_destroy(s->plan);
+        s->plan = NULL;
+    }
+    if (!s->plan) {
+        const int rc = qpp_plan_create(n > s->max_packets ? n : s->max_packets, &s->plan);
+        if (rc != QPP_OK) return rc;
+    }
+    int rc = qpp_plan_build(s->plan, kt, dd, n, s->stream);
+    if (rc == QPP_OK) rc = launch_planned(enc, kt, s->plan, dd, n, s->d_in, s->d_out, dr, s->stream);
+    return rc;
+}
+
 static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
                                  const qpp_desc *desc, uint32_t n, const uint8_t *in,
                                  size_t in_len, uint8_t *out, size_t out_len, qpp_result *res,
@@ -1570,6 +1714,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     qpp_desc *dd = (qpp_desc *)s->d_misc;
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     memcpy(hd, desc, (size_t)n * sizeof(qpp_desc));
+    reject_out_of_bounds(enc, hd, n, in_len, out_len);
     HIPCHK(hipMemcpyAsync(dd, hd, (size_t)n * sizeof(qpp_desc), hipMemcpyHostToDevice, s->s_in));
     HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     size_t olo[kPipeMaxChunks + 1];
@@ -1585,6 +1730,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         const uint32_t a = first[c], b = first[c + 1];
         size_t lo = SIZE_MAX, hi = 0;
         for (uint32_t i = a; i < b; ++i) {
+            if (hd[i].flags & kFlagReject) continue;
             const size_t o = (size_t)desc[i].in_off;
             const size_t e = o + (size_t)desc[i].hdr_len + desc[i].len + 16;
             if (o < lo) lo = o;
@@ -1599,7 +1745,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         HIPCHK(hipEventRecord(s->ev_in[c], s->s_in));
         HIPCHK(hipStreamWaitEvent(s->stream, s->ev_in[c], 0));
         if (b > a) {
-            rc = launch_packets(enc, kt, dd + a, b - a, s->d_in, s->d_out, dr + a, s->stream);
+            rc = session_launch(enc, s, kt, dd + a, b - a, dr + a);
             if (rc != QPP_OK) break;
         }
         HIPCHK(hipEventRecord(s->ev_k[c], s->stream));
@@ -1667,12 +1813,13 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
     qpp_desc *dd = (qpp_desc *)s->d_misc;
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     memcpy(hd, desc, (size_t)n * sizeof(qpp_desc));
+    reject_out_of_bounds(enc, hd, n, in_len, out_len);
     if (in_len) memcpy(s->h_in, in, in_len);
     HIPCHK(hipMemcpyAsync(dd, hd, (size_t)n * sizeof(qpp_desc), hipMemcpyHostToDevice, s->stream));
     if (in_len) HIPCHK(hipMemcpyAsync(s->d_in, s->h_in, in_len, hipMemcpyHostToDevice, s->stream));
     // bytes the kernel does not write (gaps, failed packets) come back as zeros
     if (out_len) HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
-    rc = launch_packets(enc, kt, dd, n, s->d_in, s->d_out, dr, s->stream);
+    rc = session_launch(enc, s, kt, dd, n, dr);
     if (rc != QPP_OK) return rc;
     if (out_len) HIPCHK(hipMemcpyAsync(s->h_out, s->d_out, out_len, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->stream));

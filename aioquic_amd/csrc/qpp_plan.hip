@@ -1,0 +1,170 @@
+// qpp_plan.hip -- bucketing of a packet batch by (suite, key slot) on the
+// device (quic_pp.h, qpp_plan_*).  A server's batch interleaves connections
+// (src/aioquic/asyncio/server.py:60-152); the packet kernels want each
+// workgroup on one key slot and each launch on one cipher suite, so the plan
+// sorts packet indices by (suite, slot) with a stable LSD radix sort
+// (rocPRIM) over just the bits the table's capacity needs, counts each
+// suite's bucket, and gathers descriptors into that order for every launch.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "qpp_internal.h"
+
+namespace qpp {
+
+constexpr int kPlanWG = 256;
+constexpr uint32_t kNoKeyBucket = 3;  // empty or out-of-range slot: QPP_S_NO_KEY
+
+// Sort key of packet i: bucket (suite, or 3 for no key) above the slot bits;
+// one LDS histogram per workgroup, then four global adds.
+__global__ __launch_bounds__(kPlanWG) void k_plan_keys(const KeySlot *__restrict__ slots, uint32_t cap,
+                                                       const qpp_desc *__restrict__ desc, uint32_t n,
+                                                       int slot_bits, uint32_t *__restrict__ keys,
+                                                       uint32_t *__restrict__ idx,
+                                                       uint32_t *__restrict__ count)
+{
+    __shared__ uint32_t hist[4];
+    if (threadIdx.x < 4) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kPlanWG + threadIdx.x;
+    if (i < n) {
+        const uint32_t s = desc[i].slot;
+        uint32_t b = kNoKeyBucket;
+        if (s < cap) {
+            const uint32_t suite = slots[s].suite;
+            if (suite <= QPP_CHACHA20_POLY1305) b = suite;
+        }
+        keys[i] = b << slot_bits | (s < cap ? s : 0u);
+        idx[i] = i;
+        atomicAdd(&hist[b], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 && hist[threadIdx.x]) atomicAdd(&count[threadIdx.x], hist[threadIdx.x]);
+}
+
+// count[4] -> range[8] = [begin, end) of each bucket in sorted order
+__global__ void k_plan_ranges(const uint32_t *__restrict__ count, uint32_t *__restrict__ range)
+{
+    if (threadIdx.x != 0) return;
+    uint32_t b = 0;
+    for (int s = 0; s < 4; ++s) {
+        range[2 * s] = b;
+        b += count[s];
+        range[2 * s + 1] = b;
+    }
+}
+
+// sorted[p] = desc[idx[p]], with the caller's index in rsv
+__global__ __launch_bounds__(kPlanWG) void k_plan_gather(const qpp_desc *__restrict__ desc,
+                                                         const uint32_t *__restrict__ idx, uint32_t n,
+                                                         qpp_desc *__restrict__ sorted)
+{
+    const uint32_t p = blockIdx.x * kPlanWG + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t i = idx[p];
+    qpp_desc d = desc[i];
+    d.rsv = i;
+    sorted[p] = d;
+}
+
+// Results of the no-key bucket (KeyUnavailableError, quic/crypto.py:78-79):
+// a grid-stride loop over [range[6], range[7]) with a small fixed grid.
+__global__ __launch_bounds__(kPlanWG) void k_plan_nokey(const qpp_desc *__restrict__ sorted,
+                                                        const uint32_t *__restrict__ range,
+                                                        qpp_result *__restrict__ res)
+{
+    const uint32_t b = range[2 * kNoKeyBucket], e = range[2 * kNoKeyBucket + 1];
+    for (uint32_t p = b + blockIdx.x * kPlanWG + threadIdx.x; p < e; p += gridDim.x * kPlanWG) {
+        const qpp_desc d = sorted[p];
+        res[d.rsv] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+    }
+}
+
+}  // namespace qpp
+
+using namespace qpp;
+
+static int bits_for(uint32_t cap)
+{
+    int b = 1;
+    while (b < 24 && (1u << b) < cap) ++b;
+    return b;
+}
+
+extern "C" int qpp_plan_create(uint32_t max_packets, qpp_plan **out)
+{
+    if (!out || max_packets == 0 || max_packets > (1u << 30)) return QPP_E_ARG;
+    *out = NULL;
+    qpp_plan *p = (qpp_plan *)calloc(1, sizeof(qpp_plan));
+    if (!p) return QPP_E_NOMEM;
+    p->cap = max_packets;
+    const size_t n = max_packets;
+    bool ok = hipMalloc(&p->d_keys[0], n * 4) == hipSuccess && hipMalloc(&p->d_keys[1], n * 4) == hipSuccess &&
+              hipMalloc(&p->d_idx[0], n * 4) == hipSuccess && hipMalloc(&p->d_idx[1], n * 4) == hipSuccess &&
+              hipMalloc(&p->d_sorted, n * sizeof(qpp_desc)) == hipSuccess &&
+              hipMalloc(&p->d_count, 16 * sizeof(uint32_t)) == hipSuccess;
+    if (ok) {
+        size_t tmp = 0;
+        ok = rocprim::radix_sort_pairs(nullptr, tmp, p->d_keys[0], p->d_keys[1], p->d_idx[0], p->d_idx[1],
+                                       max_packets, 0, 26) == hipSuccess &&
+             hipMalloc(&p->d_tmp, tmp ? tmp : 16) == hipSuccess;
+        p->tmp_bytes = tmp;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
+        qpp_plan_destroy(p);
+        return QPP_E_NOMEM;
+    }
+    p->d_range = p->d_count + 8;
+    *out = p;
+    return QPP_OK;
+}
+
+extern "C" void qpp_plan_destroy(qpp_plan *p)
+{
+    if (!p) return;
+    for (int i = 0; i < 2; ++i) {
+        if (p->d_keys[i]) (void)hipFree(p->d_keys[i]);
+        if (p->d_idx[i]) (void)hipFree(p->d_idx[i]);
+    }
+    if (p->d_sorted) (void)hipFree(p->d_sorted);
+    if (p->d_count) (void)hipFree(p->d_count);
+    if (p->d_tmp) (void)hipFree(p->d_tmp);
+    free(p);
+}
+
+int qpp_internal_plan_build(qpp_plan *p, const KeySlot *d_slots, uint32_t cap, const qpp_desc *d_desc,
+                            uint32_t n, hipStream_t s)
+{
+    if (n > p->cap) return QPP_E_ARG;
+    if (hipMemsetAsync(p->d_count, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return QPP_E_HIP;
+    const int sb = bits_for(cap);
+    if (n) {
+        hipLaunchKernelGGL(k_plan_keys, dim3((n + kPlanWG - 1) / kPlanWG), dim3(kPlanWG), 0, s, d_slots, cap,
+                           d_desc, n, sb, p->d_keys[0], p->d_idx[0], p->d_count);
+        size_t tmp = p->tmp_bytes;
+        if (rocprim::radix_sort_pairs(p->d_tmp, tmp, p->d_keys[0], p->d_keys[1], p->d_idx[0], p->d_idx[1], n,
+                                      0, sb + 2, s) != hipSuccess)
+            return QPP_E_HIP;
+    }
+    hipLaunchKernelGGL(k_plan_ranges, dim3(1), dim3(64), 0, s, p->d_count, p->d_range);
+    if (hipGetLastError() != hipSuccess) return QPP_E_HIP;
+    p->n_built = n;
+    return QPP_OK;
+}
+
+int qpp_internal_plan_gather(const qpp_plan *p, const qpp_desc *d_desc, uint32_t n, hipStream_t s)
+{
+    if (n != p->n_built) return QPP_E_ARG;
+    if (n == 0) return QPP_OK;
+    hipLaunchKernelGGL(k_plan_gather, dim3((n + kPlanWG - 1) / kPlanWG), dim3(kPlanWG), 0, s, d_desc,
+                       p->d_idx[1], n, p->d_sorted);
+    return hipGetLastError() == hipSuccess ? QPP_OK : QPP_E_HIP;
+}
+
+int qpp_internal_plan_nokey(const qpp_plan *p, qpp_result *d_res, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_plan_nokey, dim3(16), dim3(kPlanWG), 0, s, p->d_sorted, p->d_range, d_res);
+    return hipGetLastError() == hipSuccess ? QPP_OK : QPP_E_HIP;
+}

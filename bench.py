@@ -5,10 +5,15 @@ Metric (BASELINE.json): GiB/s of device-resident AEAD protect+unprotect on
 ranks (weak scaling: every rank owns its own shard of packets, no collective
 on the data path).  One "step" = protect the batch, then unprotect it.
 
-Default workload = BASELINE config 2: AES-128-GCM, 64Ki x 1200 B, one key.
-Other configs (--config 3/4/5) are parity/throughput cases of the same path.
+Default workload = the north-star configuration (BASELINE.json north_star):
+AES-128-GCM protect+unprotect of 1Mi x 1200 B packets, one key, per GPU.
+--config 2/3/4/5 run the other BASELINE configs.  Configs 4 and 5 arrive in
+random key order (a server socket's view of many connections), so every
+step buckets each batch by (suite, key) on the device (qpp_plan_build)
+inside the timed region, once for the protect batch and once for the
+unprotect batch.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ns] [--e2e]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 
@@ -37,23 +42,25 @@ LDS_CYCLES_PER_PKT = {0: 506.0, 1: 666.0}  # AES-128-GCM, AES-256-GCM
 N_CU, CLOCK_GHZ = 256, 2.4
 
 CONFIGS = {
-    2: dict(name="aes-128-gcm 64Ki x 1200B, 1 key", n=65536, suite=0, n_keys=1, version=1),
-    3: dict(name="chacha20-poly1305 64Ki x 1200B, 1 key, QUIC v2", n=65536, suite=2, n_keys=1,
-            version=0x6B3343CF),
-    4: dict(name="aes-256-gcm 1Mi x 1200B, 4096 keys", n=1 << 20, suite=1, n_keys=4096,
-            version=1),
-    5: dict(name="mixed aes-128-gcm/chacha20-poly1305 2Mi x 1200B per GPU", n=1 << 21, suite=0,
-            n_keys=2, version=1, mixed=(0, 2)),
+    "ns": dict(name="aes-128-gcm 1Mi x 1200B, 1 key", n=1 << 20, suite=0, n_keys=1, version=1),
+    "2": dict(name="aes-128-gcm 64Ki x 1200B, 1 key", n=65536, suite=0, n_keys=1, version=1),
+    "3": dict(name="chacha20-poly1305 64Ki x 1200B, 1 key, QUIC v2", n=65536, suite=2, n_keys=1,
+              version=0x6B3343CF),
+    "4": dict(name="aes-256-gcm 1Mi x 1200B, 4096 keys, random arrival order", n=1 << 20, suite=1,
+              n_keys=4096, version=1, order="random"),
+    "5": dict(name="mixed aes-128-gcm/chacha20-poly1305 2Mi x 1200B per GPU, 1024 keys, "
+                   "random arrival order", n=1 << 21, suite=0, n_keys=1024, version=1,
+              mixed=(0, 2), order="random"),
 }
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=100,
-                    help="untimed steps first: about 20 ms of work, which the GPU clock needs to ramp")
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first (the GPU clock needs ~20 ms of work to ramp)")
+    ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (0 = skip)")
@@ -106,35 +113,42 @@ def _cpu_loop(w, seconds: float, part: int = 0, parts: int = 1):
     if ref is None:
         sys.path.insert(0, ROOT)
         from oracle import oracle as orc
-    k = w.keys[part % len(w.keys)]
-    suite = int(k["suite"])
-    an, hn, kl = _NAMES[suite]
-    key, iv, hp = bytes(k["key"][:kl]), bytes(k["iv"]), bytes(k["hp"][:kl])
     m = min(w.n // parts, 20000)
     base = part * m
     pk = [bytes(w.plain[(base + i) * 1200 : (base + i) * 1200 + 1184]) for i in range(m)]
     pns = [int(x) for x in w.desc["pn"][base : base + m]]
+    slots = [int(x) for x in w.desc["slot"][base : base + m]]
+    # each sampled packet under its own connection's key (per-connection
+    # objects, built before timing, as aioquic builds them at key install)
+    objs = {}
+    for sl in set(slots):
+        k = w.keys[sl]
+        suite = int(k["suite"])
+        an, hn, kl = _NAMES[suite]
+        key, iv, hp = bytes(k["key"][:kl]), bytes(k["iv"]), bytes(k["hp"][:kl])
+        if ref is not None:
+            objs[sl] = (ref.AEAD(an, key, iv), ref.HeaderProtection(hn, hp))
+        else:
+            objs[sl] = (suite, key, iv, hp)
+    ko = [objs[sl] for sl in slots]
     done = 0
     t_p = t_u = 0.0
     t_end = time.perf_counter() + seconds
-    if ref is not None:
-        aead = ref.AEAD(an, key, iv)
-        hpo = ref.HeaderProtection(hn, hp)
     while time.perf_counter() < t_end:
         t0 = time.perf_counter()
         if ref is not None:
-            wire = [hpo.apply(p[:11], aead.encrypt(p[11:], p[:11], pn)) for p, pn in zip(pk, pns)]
+            wire = [o[1].apply(p[:11], o[0].encrypt(p[11:], p[:11], pn)) for p, pn, o in zip(pk, pns, ko)]
         else:
-            wire = [orc.protect(suite, key, iv, hp, p[:11], p[11:], pn) for p, pn in zip(pk, pns)]
+            wire = [orc.protect(o[0], o[1], o[2], o[3], p[:11], p[11:], pn) for p, pn, o in zip(pk, pns, ko)]
         t1 = time.perf_counter()
         if ref is not None:
-            for x, pn in zip(wire, pns):
-                hdr, trunc = hpo.remove(x, 9)
+            for x, pn, o in zip(wire, pns, ko):
+                hdr, trunc = o[1].remove(x, 9)
                 pnd = decode_packet_number(trunc, ((hdr[0] & 3) + 1) * 8, pn)
-                aead.decrypt(x[len(hdr):], hdr, pnd)
+                o[0].decrypt(x[len(hdr):], hdr, pnd)
         else:
-            for x, pn in zip(wire, pns):
-                orc.unprotect(suite, key, iv, hp, x, 9, pn)
+            for x, pn, o in zip(wire, pns, ko):
+                orc.unprotect(o[0], o[1], o[2], o[3], x, 9, pn)
         t2 = time.perf_counter()
         t_p += t1 - t0
         t_u += t2 - t1
@@ -171,9 +185,9 @@ def cpu_baseline(w, seconds: float, cfg, procs: int = 1):
         done = sum(r[0] for r in res)
         kind = res[0][2]
         value = sum(r[0] * 1200 / r[1] for r in res) / GIB
-    an = _NAMES[int(w.keys[0]["suite"])][0].decode()
+    an = "/".join(sorted({_NAMES[int(s)][0].decode() for s in w.suites[: min(w.n, 20000)]}))
     return {"value": round(value, 4), "unit": "GiB/s", "cores": procs, "kind": kind,
-            "sample": f"{done} packets of the bench workload ({cfg['name']}), suite {an}, "
+            "sample": f"{done} packets of the bench workload ({cfg['name']}), suites {an}, "
                       f"per-packet {'aioquic _crypto.c + OpenSSL' if kind == 'reference' else 'C oracle'}"
                       f" calls, ~{seconds:.0f} s on {procs} core(s) of the GPU host"}
 
@@ -310,11 +324,15 @@ def main():
 
     # shard: rank r owns packets [r*n, (r+1)*n) of the global stream
     first, n = shard_range(rank, world, n)
-    w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=0x9001 + args.config,
-                      version=cfg["version"], mixed=cfg.get("mixed"), first_packet=first)
-    # the CPU baselines run before anything touches the GPU (they fork)
+    seed = 0x9001 + (int(args.config) if args.config.isdigit() else 0)
+    w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=seed,
+                      version=cfg["version"], mixed=cfg.get("mixed"), first_packet=first,
+                      order=cfg.get("order", "grouped"))
+    bucketed = cfg.get("order", "grouped") != "grouped"
+    # the CPU baselines run before anything touches the GPU (they fork); at
+    # N > 1 rank 0 times them while the other ranks wait at the first barrier
     cpu = cpu_all = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         cpu = cpu_baseline(w, args.cpu_seconds, cfg, 1)
         if args.cpu_all_cores:
             cpu_all = cpu_baseline(w, max(2.0, args.cpu_seconds / 2), cfg, cpu_share())
@@ -343,14 +361,23 @@ def main():
     hev = HipEvents(torch)
 
     def step(ev=None):
+        # bucketed configs: each batch is sorted by (suite, key) on the device
+        # first -- the protect batch and the unprotect batch each get their own
+        # plan build, as two independent batches of a server would
         if ev:
             hev.record(ev[0], stream)
-        eng.protect(d_desc, n, d_plain, d_wire, d_r1, stream)
+        plan = eng.bucket(d_desc, n, stream) if bucketed else None
         if ev:
             hev.record(ev[1], stream)
-        eng.unprotect(d_udesc, n, d_wire, d_back, d_r2, stream)
+        eng.protect(d_desc, n, d_plain, d_wire, d_r1, stream, plan)
         if ev:
             hev.record(ev[2], stream)
+        plan = eng.bucket(d_udesc, n, stream) if bucketed else None
+        if ev:
+            hev.record(ev[3], stream)
+        eng.unprotect(d_udesc, n, d_wire, d_back, d_r2, stream, plan)
+        if ev:
+            hev.record(ev[4], stream)
 
     for _ in range(args.warmup):
         step()
@@ -361,7 +388,7 @@ def main():
     # for the roofline).  Sampling keeps the events' own stream time (a few us
     # per record) out of most steps of `value`.
     every = max(1, args.event_every)
-    evs = [[hev.new() for _ in range(3)] if k % every == 0 else None for k in range(args.steps)]
+    evs = [[hev.new() for _ in range(5)] if k % every == 0 else None for k in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -378,8 +405,9 @@ def main():
     elapsed = float(t.item())
 
     evs = [e for e in evs if e]
-    t_prot = float(np.mean([hev.ms(e[0], e[1]) for e in evs])) / 1e3
-    t_unp = float(np.mean([hev.ms(e[1], e[2]) for e in evs])) / 1e3
+    t_plan = float(np.mean([hev.ms(e[0], e[1]) + hev.ms(e[2], e[3]) for e in evs])) / 1e3
+    t_prot = float(np.mean([hev.ms(e[1], e[2]) for e in evs])) / 1e3
+    t_unp = float(np.mean([hev.ms(e[3], e[4]) for e in evs])) / 1e3
     hev_flags = hev.flags
     hev.close()
 
@@ -421,8 +449,11 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded 1-RTT packets, 11 B header + 1173 B payload + 16 B tag)",
             "config": {"workload": _workload_name(cfg, n), "packets_per_gpu": n, "packet_bytes": 1200,
-                       "keys": w.n_keys, "parallelism": f"packet shards x{world}"},
-            "kernels_ms": {"protect": round(t_prot * 1e3, 4), "unprotect": round(t_unp * 1e3, 4)},
+                       "keys": w.n_keys, "arrival": cfg.get("order", "grouped"),
+                       "bucketed_in_timed_region": bucketed,
+                       "parallelism": f"packet shards x{world}"},
+            "kernels_ms": {"protect": round(t_prot * 1e3, 4), "unprotect": round(t_unp * 1e3, 4),
+                           "bucketing": round(t_plan * 1e3, 4) if bucketed else None},
             "kernel_gib_s": round(n * 1200 / (t_prot + t_unp) / GIB, 3),
             "event_flags": hex(hev_flags), "event_steps": len(evs),
             "roofline": {"bound": "hbm", "kernel": dom, "launch_us": round(kern_t * 1e6, 2),
@@ -442,7 +473,7 @@ def main():
         if w.n_keys >= 64:
             out["key_schedule"] = key_schedule(PacketEngine, w.n_keys, cfg["suite"], cfg["version"])
         if args.e2e:
-            out["e2e"] = e2e(PacketEngine, cfg, 0x9001 + args.config, dev, args.e2e_packets,
+            out["e2e"] = e2e(PacketEngine, cfg, seed, dev, args.e2e_packets,
                              chunks=args.e2e_chunks, n_streams=args.e2e_streams,
                              mode=args.e2e_mode)
         print(json.dumps(out), flush=True)

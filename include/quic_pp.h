@@ -11,8 +11,26 @@
  *
  * Threading: a qpp_keytab may be shared between threads for launches; setting
  * keys and launching on the same slots concurrently is the caller's race (as
- * with the reference's per-object scratch, _crypto.c:39-42).  A qpp_session is
- * single-threaded.
+ * with the reference's per-object scratch, _crypto.c:39-42).  A qpp_session and
+ * a qpp_plan are single-threaded: use one per thread (the CPython binding
+ * keeps one session per OS thread).
+ *
+ * Buffers: the device-pointer launches (qpp_protect, qpp_unprotect and the
+ * planned forms) cannot see buffer sizes, so every descriptor's input and
+ * output extents must lie inside the caller's allocations, and the 16
+ * packets of one wavefront (consecutive descriptors, or consecutive in a
+ * plan's bucket order) must lie within 4 GiB of each other (else
+ * QPP_S_LENGTH).  The session forms check every descriptor against in_len /
+ * out_len and report QPP_S_LENGTH for one that does not fit, without touching
+ * memory for it.
+ *
+ * Authentication failures: unprotect decrypts as it authenticates, so the
+ * plaintext of a packet whose tag does not verify is produced before the
+ * verdict.  The kernels then overwrite that packet's payload region at
+ * out_off + hdr_len with zeros (out_len = 0), so no unauthenticated plaintext
+ * is left in the output.  An in-place unprotect (in == out) of a forged
+ * packet therefore also destroys its ciphertext, as the reference's copy-out
+ * semantics never do (_crypto.c:145-154 returns an error, not bytes).
  */
 #ifndef QUIC_PP_H
 #define QUIC_PP_H
@@ -24,7 +42,7 @@
 extern "C" {
 #endif
 
-#define QPP_ABI_VERSION 1
+#define QPP_ABI_VERSION 2
 
 /* cipher suites (quic/crypto.py:12-16 CIPHER_SUITES) */
 #define QPP_AES_128_GCM 0        /* aes-128-gcm + aes-128-ecb header protection */
@@ -144,6 +162,30 @@ int qpp_protect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n, const 
                 uint8_t *d_out, qpp_result *d_res, void *stream);
 int qpp_unprotect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                   const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream);
+
+/* Bucketing by (suite, key slot).  A server's batch interleaves many
+ * connections (src/aioquic/asyncio/server.py:60-152 demultiplexes them per
+ * datagram), but a kernel wants each workgroup on one key and one suite.
+ * qpp_plan_build sorts the batch's packet indices on the device by
+ * (suite, slot), stable within a bucket, and counts the packets of each
+ * suite.  A *_planned launch gathers its descriptors into that order, runs
+ * each suite's kernel over its own bucket only, and writes every result at
+ * the packet's position in the CALLER's descriptor order.  A plan is built
+ * once per batch and serves every launch over descriptors with the same
+ * slots in the same positions (e.g. protect, then unprotect of the same
+ * packets).  Asynchronous on `stream`; a plan serves one stream at a time.
+ * Empty or unknown slots are reported QPP_S_NO_KEY, as by qpp_protect. */
+typedef struct qpp_plan qpp_plan;
+int qpp_plan_create(uint32_t max_packets, qpp_plan **out);
+void qpp_plan_destroy(qpp_plan *p);
+int qpp_plan_build(qpp_plan *p, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
+                   void *stream);
+int qpp_protect_planned(const qpp_keytab *kt, const qpp_plan *p, const qpp_desc *d_desc,
+                        uint32_t n, const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res,
+                        void *stream);
+int qpp_unprotect_planned(const qpp_keytab *kt, const qpp_plan *p, const qpp_desc *d_desc,
+                          uint32_t n, const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res,
+                          void *stream);
 
 /* Header-protection masks: replaces HeaderProtection_mask (_crypto.c:278-287).
  * d_samples: n x 16 bytes, d_masks: n x 16 bytes (first 5 used). */

@@ -193,3 +193,42 @@ def test_receive_batch_many_connections():
     assert rb.launches == 1
     for (sv, off, pn, hdr, payload), o in zip(meta, got):
         assert o == (hdr, payload, pn)
+
+
+@pytest.mark.parametrize("suite", SUITES)
+def test_receive_batch_one_byte_pns_past_the_window(suite):
+    """More than 256 packets of one connection with 1-byte packet numbers: a
+    packet decoded under the batch's starting expected number would get the
+    wrong packet number (pn 256 decodes as 0), fail authentication and be
+    dropped, though the sequential decrypt_packet accepts it once earlier
+    packets have advanced expected_packet_number (batch_io.py)."""
+    from aioquic_amd.batch_io import ReceiveBatch
+
+    rng = np.random.default_rng(61)
+    (cl, sv), (_, sv2) = _pairs(rng, suite)
+    pkts = []
+    for pn in range(300):
+        hdr = _short_header(0, pn, pn_len=1)
+        pkts.append(cl.encrypt_packet(hdr, rng.bytes(int(rng.integers(8, 200))), pn))
+    b = bytearray(pkts[200])
+    b[-1] ^= 1
+    pkts[200] = bytes(b)
+
+    class Space:
+        expected_packet_number = 0
+
+    sp, sp2 = Space(), Space()
+    batch = ReceiveBatch(capacity=8)
+    for pkt in pkts:
+        batch.add(sv, pkt, 9, space=sp)
+    got = [(("ok",) + tuple(o)) if isinstance(o, tuple) else (type(o).__name__, str(o))
+           for o in batch.run()]
+    want = []
+    for pkt in pkts:
+        o = _outcome(lambda: sv2.decrypt_packet(pkt, 9, sp2.expected_packet_number))
+        if o[0] == "ok" and o[3] > sp2.expected_packet_number:
+            sp2.expected_packet_number = o[3] + 1
+        want.append(o)
+    assert got == want
+    assert sum(o[0] == "ok" for o in got) == 299
+    assert sp.expected_packet_number == sp2.expected_packet_number == 300
