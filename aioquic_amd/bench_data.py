@@ -83,11 +83,14 @@ def _per_key_counter(key_of: np.ndarray, n_keys: int) -> np.ndarray:
 
 def make_workload(n: int, suite=L.AES_128_GCM, n_keys: int = 1, seed: int = 0x9001,
                   version: int = QuicProtocolVersion.VERSION_1, mixed=None,
-                  first_packet: int = 0, order: str = "grouped") -> Workload:
+                  first_packet: int = 0, order: str = "grouped",
+                  layout: str = "arrival") -> Workload:
     """n packets; `mixed` = list of suites (config 5): keys get a seeded
     random suite from it with order="random", else round-robin; without
     `mixed` every key uses `suite`.  `first_packet` offsets a rank's shard
-    in the global stream."""
+    in the global stream.  layout="by_key" stores the packets of one key
+    contiguously in memory whatever the arrival order (a study knob: it
+    separates the cost of scattered memory from the cost of bucketing)."""
     suites = list(mixed) if mixed else [suite]
     keys = make_keys(n_keys, suites, seed, int(version), random_suites=order == "random")
     rng = np.random.default_rng(seed + 1)
@@ -116,7 +119,15 @@ def make_workload(n: int, suite=L.AES_128_GCM, n_keys: int = 1, seed: int = 0x90
     view[:, HDR_LEN : HDR_LEN + PAYLOAD_LEN] = rng.integers(0, 256, size=(n, PAYLOAD_LEN),
                                                             dtype=np.uint8)
 
-    offs = np.arange(n, dtype=np.uint64) * SLOT_BYTES
+    if layout == "by_key":
+        pos = np.empty(n, np.int64)
+        pos[np.argsort(key_of, kind="stable")] = np.arange(n)
+        offs = pos.astype(np.uint64) * SLOT_BYTES
+        view[pos] = view.copy()
+    elif layout == "arrival":
+        offs = np.arange(n, dtype=np.uint64) * SLOT_BYTES
+    else:
+        raise ValueError(f"unknown layout {layout!r}")
     desc = np.zeros(n, dtype=L.DESC)
     desc["in_off"] = offs
     desc["out_off"] = offs

@@ -75,7 +75,8 @@ static_assert(sizeof(KeySlot) == 768, "KeySlot layout");
 // GHASH tables of one slot: [power p = H^(p+1)][window w][nibble v] -> 16 bytes.
 // Window w = 2*byte + (0: low nibble, 1: high nibble).  32 KiB per slot.
 constexpr int kGhashPowers = 4;
-constexpr int kGhashTabBytes = kGhashPowers * 32 * 16 * 16;
+constexpr int kGhashPowBytes = 32 * 16 * 16;  // one power: 32 windows x 16 nibbles x 16 B
+constexpr int kGhashTabBytes = kGhashPowers * kGhashPowBytes;
 
 // ---------------------------------------------------------------- helpers --
 
@@ -473,6 +474,87 @@ __device__ __forceinline__ u32x4 ghash_mul(u32x4 x, const uint8_t *lds, uint32_t
             uint32_t ahi = __builtin_amdgcn_perm(0u, hi, sel);
             u32x4 e0 = *(const u32x4 *)(lds + tab + wlo * 256 + alo);
             u32x4 e1 = *(const u32x4 *)(lds + tab + whi * 256 + ahi);
+            acc = xor3(acc, e0, e1);
+        }
+    }
+    return acc;
+}
+
+// x * H^p with the table of one power chosen at run time among the
+// workgroup's resident tables: tables of 8 KiB at LDS offsets r * 8192 from
+// `base` (r < 8); tsel = r * 8192.  The table offset rides in byte 1 of the
+// same v_perm that extracts the nibble, so the selection costs no instruction.
+__device__ __forceinline__ u32x4 ghash_mul_lds(u32x4 x, const uint8_t *base, uint32_t tsel)
+{
+    u32x4 acc = {0, 0, 0, 0};
+    uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t hi = xw[d] & 0xF0F0F0F0u;
+        uint32_t lo = (xw[d] << 4) & 0xF0F0F0F0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int wlo = 2 * (4 * d + b), whi = wlo + 1;
+            // byte 0: nibble * 16 (byte b of lo / hi), byte 1: tsel byte 1
+            const uint32_t sel = 0x0c0c0500u | (uint32_t)b;
+            uint32_t alo = __builtin_amdgcn_perm(tsel, lo, sel);
+            uint32_t ahi = __builtin_amdgcn_perm(tsel, hi, sel);
+            u32x4 e0 = *(const u32x4 *)(base + wlo * 256 + alo);
+            u32x4 e1 = *(const u32x4 *)(base + whi * 256 + ahi);
+            acc = xor3(acc, e0, e1);
+        }
+    }
+    return acc;
+}
+
+// The same, one input word (8 reads, 32 VGPRs in flight) at a time: for the
+// multiplies outside the step loop, where all 32 reads in flight would not
+// fit beside the live packet state.
+__device__ __forceinline__ u32x4 ghash_mul_lds_narrow(u32x4 x, const uint8_t *base, uint32_t tsel)
+{
+    u32x4 acc = {0, 0, 0, 0};
+    uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll 1
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t wd = d == 0 ? xw[0] : d == 1 ? xw[1] : d == 2 ? xw[2] : xw[3];
+        uint32_t hi = wd & 0xF0F0F0F0u;
+        uint32_t lo = (wd << 4) & 0xF0F0F0F0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int wlo = 2 * (4 * d + b), whi = wlo + 1;
+            const uint32_t sel = 0x0c0c0500u | (uint32_t)b;
+            uint32_t alo = __builtin_amdgcn_perm(tsel, lo, sel);
+            uint32_t ahi = __builtin_amdgcn_perm(tsel, hi, sel);
+            u32x4 e0 = *(const u32x4 *)(base + wlo * 256 + alo);
+            u32x4 e1 = *(const u32x4 *)(base + whi * 256 + ahi);
+            acc = xor3(acc, e0, e1);
+        }
+    }
+    return acc;
+}
+
+// x * H^p from the slot's tables in global memory (tab = that power's 8 KiB):
+// the few multiplies per packet outside the step loop (associated-data fold,
+// the last step's H^(4-j)).  32 independent 16-byte loads, L1/L2 hits.
+__device__ __forceinline__ u32x4 ghash_mul_global(u32x4 x, const uint8_t *tab)
+{
+    u32x4 acc = {0, 0, 0, 0};
+    uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+    // one input word (8 loads, 32 VGPRs in flight) at a time: all 32 loads at
+    // once would hold 128 VGPRs and spill in the 128-VGPR kernels
+#pragma unroll 1
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t w = d == 0 ? xw[0] : d == 1 ? xw[1] : d == 2 ? xw[2] : xw[3];
+        uint32_t hi = w & 0xF0F0F0F0u;
+        uint32_t lo = (w << 4) & 0xF0F0F0F0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int wlo = 2 * (4 * d + b), whi = wlo + 1;
+            const uint32_t sel = 0x0c0c0c00u | (uint32_t)b;
+            const uint32_t alo = __builtin_amdgcn_perm(0u, lo, sel);
+            const uint32_t ahi = __builtin_amdgcn_perm(0u, hi, sel);
+            u32x4 e0 = *(const u32x4 *)(tab + wlo * 256 + alo);
+            u32x4 e1 = *(const u32x4 *)(tab + whi * 256 + ahi);
             acc = xor3(acc, e0, e1);
         }
     }

@@ -54,9 +54,6 @@ constexpr bool kBalance = QPP_BALANCE;  // GCM wave balancing (s_setprio)
 #define QPP_BALANCE_ENC 1
 #endif
 constexpr bool kBalanceEnc = QPP_BALANCE_ENC;  // ... for protect too
-#ifndef QPP_FUSE_GH
-#define QPP_FUSE_GH 0  // GCM: weave a step's H^4 product into the next block's AES (measured slower)
-#endif
 #ifndef QPP_VMCNT1
 #define QPP_VMCNT1 0  // GCM step loop: wait for the LDS-DMA only, not the last store (no gain)
 #endif
@@ -68,43 +65,8 @@ constexpr bool kBalanceEnc = QPP_BALANCE_ENC;  // ... for protect too
 #endif
 
 template <int WG>
-struct __attribute__((aligned(16))) GcmSmem {
-    // GHASH tables first: every table offset (< 32 KiB) and the AES image
-    // base (32 KiB) then fit the 16-bit ds_read immediate
-    uint8_t gt[kGhashTabBytes];       // GHASH H^1..H^4 tables      32 KiB
-    uint8_t te[kTeBytes];             // Te0|Te1 x 32 bank copies   64 KiB
-    uint8_t scratch[WG / 4][kScratch];
-    uint8_t stage[WG / 64][2][kStageBytes];  // per-wave LDS-DMA input staging
-    KeySlot kslot;                           // the current key slot (LDS-DMA)
-    uint32_t cur_slot[2];
-    uint32_t progress;  // steps done by the workgroup's waves (wave balancing)
-};
-
-// LDS-DMA of key slot s (768 B) and its GHASH tables (32 KiB) into a GCM
-// workgroup's LDS: one 1 KiB chunk per wave instruction.  The caller retires
-// it with s_waitcnt vmcnt(0) before the barrier that precedes any use.
-template <int WG>
-__device__ __forceinline__ void stage_key(GcmSmem<WG> &sm, const KeySlot *slots,
-                                          const uint8_t *gtab, uint32_t s)
-{
-    typedef const __attribute__((address_space(1))) void *gptr_t;
-    typedef __attribute__((address_space(3))) void *lptr_t;
-    // wave index as an SGPR and a fresh lane id: this also runs inside the
-    // packet loops, where a kept lane address would be spilled
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = (int)lane_fresh();
-    const uint8_t *gt = gtab + (size_t)s * kGhashTabBytes;
-    for (int c = w; c < kGhashTabBytes / 1024; c += WG / 64)
-        __builtin_amdgcn_global_load_lds((gptr_t)(gt + c * 1024 + l * 16), (lptr_t)(sm.gt + c * 1024),
-                                         16, 0, 0);
-    if (w == 0 && l < (int)(sizeof(KeySlot) / 16))
-        __builtin_amdgcn_global_load_lds((gptr_t)((const uint8_t *)(slots + s) + l * 16),
-                                         (lptr_t)&sm.kslot, 16, 0, 0);
-}
-
-template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
     uint8_t scratch[WG / 4][kScratch];
-    uint32_t cur_slot[2];
 };
 
 // Fill the LDS AES image: row x = [Te0[x] x 32 | Te1[x] x 32], 16-byte stores.
@@ -478,10 +440,26 @@ __device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, ui
 // staging slot, packet scratch) is recomputed from lane_fresh(): 128 VGPRs
 // leave no room to keep them live.  scr_wave = the wave's 16 packet
 // scratches, stage = the wave's 2 staging buffers, te = the AES image.
+// GHASH tables of the packet's key slot in LDS: four 8 KiB buffers at LDS
+// offset 0 (ghash_mul_lds selects one in its v_perm).  The wave's table word
+// (in LDS, re-read where needed rather than kept in SGPRs) says which buffer
+// holds H^1 (bits 0-3) and H^4 (bits 4-7); bit 8: all four powers are
+// resident (buffer p = H^(p+1)), so the last step can multiply every lane by
+// its own H^(4-j).
+struct GhashTabs {
+    const uint8_t *base;
+    const uint32_t *wtab;
+    __device__ __forceinline__ uint32_t word() const
+    {
+        return __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)wtab);
+    }
+};
+constexpr uint32_t kTabAll = 0x100u;
+
 template <int NR, bool ENC>
 __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int clen,
                                             const uint32_t *rk, int sub, uint8_t *scr,
-                                            uint8_t *scr_wave, const uint8_t *lds,
+                                            uint8_t *scr_wave, const GhashTabs &G,
                                             const uint8_t *te, const Bufs &B,
                                             const uint8_t *src, uint32_t ioff, uint32_t ooff,
                                             const u32x4 hmask, const uint32_t hbits, const u32x4 h0,
@@ -492,7 +470,9 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     const int n_g = za + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
     const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
     const bool tiny = rlen < 16;
-    constexpr uint32_t kTabH4 = 3 * 8192;
+    // the H^4 buffer, read once: an LDS read inside the step loop would make
+    // every step wait for all of its outstanding table lookups
+    const uint32_t t4 = ((G.word() >> 4) & 15u) * (uint32_t)kGhashPowBytes;
 
     if (tiny) *(u32x4 *)(scr + kScrTail) = ld_part(src, rlen);
 
@@ -513,7 +493,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         a = keep_bytes(a, min(16, hlen - 16 * g));
         if (!ENC && (hbits >> 28))
             a ^= hp_pattern(16 * g, hmask, hbits & 0xff, (hbits >> 8) & 0xffff, (hbits >> 24) & 0xf);
-        if (g > 0) z = ghash_mul(z, lds, 0);
+        if (g > 0) z = ghash_mul_lds_narrow(z, G.base, (G.word() & 15u) * (uint32_t)kGhashPowBytes);  // H^1
         z ^= a;
     }
     u32x4 acc = (za && sub == pad) ? z : u32x4{0, 0, 0, 0};
@@ -530,17 +510,8 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     auto step = [&](int i, bool last, bool first, u32x4 raw) {
         const bool is_ct = i >= 0 && 16 * i < clen;
         const LdsTe Tl{te, (lane_fresh() & 31) * 4};
-#if QPP_FUSE_GH
-        // the previous steps' H^4 product rides on this block's AES phases
-        // (the first step's product is discarded: acc holds Z or 0 there)
-        u32x4 gm;
-        const u32x4 ksb =
-            aes_ctr_gh<NR>(cc, is_ct ? (uint32_t)(i + 2) : 1u, rk, Tl, acc, lds, kTabH4, gm);
-        if (!first) acc = gm;
-#else
         (void)first;
         const u32x4 ksb = aes_ctr<NR>(cc, is_ct ? (uint32_t)(i + 2) : 1u, rk, Tl);
-#endif
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
         uint32_t soff = kOob;
         if (is_ct) {
@@ -559,14 +530,10 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         }
         __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
         acc ^= x;
-#if !QPP_FUSE_GH
         __builtin_amdgcn_sched_barrier(0);
-        // H^4 inside the loop (table offset folds into the ds_read immediates);
-        // the last step's H^(4-j) is applied after the loop
-        if (!last) acc = ghash_mul(acc, lds, kTabH4);
-#else
-        (void)last;
-#endif
+        // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
+        // is applied after the loop
+        if (!last) acc = ghash_mul_lds(acc, G.base, t4);
     };
     // buffer offset of CT block i's input (or out of range)
     auto ct_load = [&](int i) -> uint32_t {
@@ -627,11 +594,33 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     }
     // lane-derived values recomputed after the loop rather than kept (spilled)
     const uint32_t lf = lane_fresh();
-    acc = ghash_mul(acc, lds, (uint32_t)(3 - (lf & 3)) * 8192u);
-    // the lengths block is the last of the sequence: lane 3, last step
+    const uint32_t tw = G.word();
+    if (tw & kTabAll) {
+        // every power resident: lane j multiplies by H^(4-j) (buffer 3 - j)
+        acc = ghash_mul_lds_narrow(acc, G.base, (uint32_t)(3 - (lf & 3)) * (uint32_t)kGhashPowBytes);
+        // the lengths block is the last of the sequence: lane 3, last step
+        __builtin_amdgcn_wave_barrier();
+        if ((lf & 3) == 3) acc ^= *(const u32x4 *)(scr_wave + (lf >> 2) * kScratch + kScrEj0);
+        return quad_xor_all(acc);
+    }
+    // H^1 and H^4 only: sum_j acc_j H^(4-j) = (((acc_0 H + acc_1) H + acc_2) H + acc_3) H,
+    // one step per lane of the quad, lane 3 ending with the sum
+    const uint32_t t1 = (tw & 15u) * (uint32_t)kGhashPowBytes;
+    u32x4 t = zero4();
+#pragma unroll 1
+    for (int j = 0; j < 4; ++j) {
+        u32x4 prev;  // lane i <- lane i-1's t, lane 0 <- 0
+        prev.x = quad_perm<0x90>(t.x);
+        prev.y = quad_perm<0x90>(t.y);
+        prev.z = quad_perm<0x90>(t.z);
+        prev.w = quad_perm<0x90>(t.w);
+        if ((lane_fresh() & 3) == 0) prev = zero4();
+        t = ghash_mul_lds_narrow(prev ^ acc, G.base, t1);
+    }
     __builtin_amdgcn_wave_barrier();
-    if ((lf & 3) == 3) acc ^= *(const u32x4 *)(scr_wave + (lf >> 2) * kScratch + kScrEj0);
-    return quad_xor_all(acc);
+    const uint32_t l2 = lane_fresh();
+    if ((l2 & 3) == 3) t ^= *(const u32x4 *)(scr_wave + (l2 >> 2) * kScratch + kScrEj0);
+    return u32x4{quad_perm<0xFF>(t.x), quad_perm<0xFF>(t.y), quad_perm<0xFF>(t.z), quad_perm<0xFF>(t.w)};
 }
 
 // Output side of a GCM packet after the step loop: partial tail block, tag,
@@ -840,191 +829,353 @@ __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int su
 
 // ---------------------------------------------------------------- kernels --
 
-// One kernel per cipher suite: a launch handles the packets whose key slot
-// holds SUITE and leaves the others to the launch of their suite (the host
-// launches one kernel per suite present in the table).  Register allocation
-// is then sized for one cipher, not the union of three.
-template <int SUITE, int WG>
-using SuiteSmem =
-    typename std::conditional<SUITE == QPP_CHACHA20_POLY1305, ChachaSmem<WG>, GcmSmem<WG>>::type;
+// ---------------------------------------------------------------- kernels --
+//
+// One kernel per cipher suite and direction: a launch handles the packets
+// whose key slot holds SUITE and leaves the others to the launch of their
+// suite.  Register allocation is then sized for one cipher.
+//
+// Unplanned launch: positions [0, n) of desc, 16 per wave, result of
+// position p at res[p].  Planned launch (items != null): desc is the plan's
+// bucket-ordered copy, each wave takes one item of this suite's items
+// [irange[2 SUITE], irange[2 SUITE + 1]) (wave_span), and a packet's result
+// goes to res[desc.rsv] (its index in the caller's order).
 
+// GCM: the workgroup's 32 KiB of GHASH table buffers hold either all four
+// powers of its one key slot, or H^1 and H^4 of each of its two lowest slots,
+// so the waves of a workgroup whose 256 packets span two connections (a
+// bucketed server batch: ~2 slots per workgroup at 4096 keys per Mi packets)
+// each run their own slot without waiting for the others.  Further slots
+// (rare once bucketed) run one after the other through buffers 0 and 1.
+constexpr int kResident = 2;
+
+template <int WG>
+struct __attribute__((aligned(16))) GcmSmem {
+    // GHASH table buffers first (LDS offset 0: ghash_mul_lds adds b * 8 KiB in
+    // its v_perm), then the AES image at 32 KiB; both within the 16-bit
+    // ds_read immediate range
+    uint8_t h4[4][kGhashPowBytes];           // 32 KiB
+    uint8_t te[kTeBytes];                    // Te0|Te1 x 32 bank copies   64 KiB
+    uint8_t scratch[WG / 4][kScratch];
+    uint8_t stage[WG / 64][2][kStageBytes];  // per-wave LDS-DMA input staging
+    uint32_t resident[kResident];            // slots of the resident tables (kNoSlot: none)
+    uint32_t wslot[WG / 64];                 // per wave: the slot it is running
+    uint32_t wtab[WG / 64];                  // per wave: its GhashTabs word
+    uint32_t wlast[WG / 64];                 // per wave: the last slot it ran
+    uint32_t more;                           // lowest slot beyond the resident ones (fallback)
+    uint32_t cur[2];                         // fallback: the slot being run / the next one
+    uint32_t progress;                       // steps done by the workgroup's waves (wave balancing)
+};
+
+// LDS-DMA of slot s's table of H^(p+1) (8 KiB) into table buffer r: 1 KiB
+// pieces spread over the workgroup's waves.  Retired by the caller
+// (vmcnt(0) + barrier) before use.
+template <int WG>
+__device__ __forceinline__ void stage_pow(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t s, int p, int r,
+                                          int w0)
+{
+    typedef const __attribute__((address_space(1))) void *gptr_t;
+    typedef __attribute__((address_space(3))) void *lptr_t;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = (int)lane_fresh();
+    const uint8_t *src = gtab + (size_t)s * kGhashTabBytes + p * kGhashPowBytes;
+    for (int c = (w + w0) % (WG / 64); c < kGhashPowBytes / 1024; c += WG / 64)
+        __builtin_amdgcn_global_load_lds((gptr_t)(src + c * 1024 + l * 16), (lptr_t)(sm.h4[r] + c * 1024),
+                                         16, 0, 0);
+}
+
+// The packets of one wave: positions [b, e) of desc.  Unplanned: 16
+// consecutive positions per wave.  Planned: the wave's item of the plan (<= 16
+// positions on one key slot, qpp_plan.hip), so that no wave straddles two
+// slots -- a straddling wave runs its packets in two passes and holds its
+// workgroup (one per CU) for twice as long.  empty_wg: the whole workgroup is
+// past the batch / the suite's items (uniform, so it may return before any
+// barrier).
+struct WaveSpan {
+    uint32_t b, e;
+    bool empty_wg;
+};
+template <int WG, int SUITE>
+__device__ __forceinline__ WaveSpan wave_span(uint32_t n, const uint32_t *items, const uint32_t *irange,
+                                              uint32_t wv)
+{
+    constexpr uint32_t kWaves = WG / 64;
+    WaveSpan w{0u, 0u, false};
+    if (irange) {
+        const uint32_t ib = irange[2 * SUITE], ie = irange[2 * SUITE + 1];
+        const uint32_t j0 = ib + blockIdx.x * kWaves;
+        w.empty_wg = j0 >= ie;
+        const uint32_t j = j0 + wv;
+        if (j < ie) {
+            w.b = __builtin_amdgcn_readfirstlane(items[j]);
+            w.e = __builtin_amdgcn_readfirstlane(items[j + 1]);
+        }
+    } else {
+        const uint32_t b0 = blockIdx.x * (kWaves * 16u);
+        w.empty_wg = b0 >= n;
+        w.b = b0 + wv * 16u;
+        w.e = w.b < n ? min(n, w.b + 16u) : w.b;
+    }
+    return w;
+}
 
 template <int SUITE, bool ENC, int WG>
-__global__ __launch_bounds__(WG, (SUITE == QPP_CHACHA20_POLY1305 ? QPP_CHACHA_WPE : 1)) void k_packets(const KeySlot *__restrict__ slots,
-                                                const uint8_t *__restrict__ gtab, uint32_t cap,
-                                                const qpp_desc *__restrict__ desc, uint32_t n,
-                                                const uint8_t *gin, uint8_t *gout,
-                                                qpp_result *__restrict__ res,
-                                                const uint32_t *__restrict__ range)
+__global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots,
+                                              const uint8_t *__restrict__ gtab, uint32_t cap,
+                                              const qpp_desc *__restrict__ desc, uint32_t n,
+                                              const uint8_t *gin, uint8_t *gout,
+                                              qpp_result *__restrict__ res,
+                                              const uint32_t *__restrict__ items,
+                                              const uint32_t *__restrict__ irange)
 {
-    constexpr bool kGcm = SUITE != QPP_CHACHA20_POLY1305;
     constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
-    constexpr int kPktPerWG = WG / 4;
-    // Planned launch (range != null): desc is the plan's bucket-ordered copy,
-    // this suite's packets are positions [range[2 SUITE], range[2 SUITE + 1]),
-    // and a packet's result goes to res[desc.rsv] (its index in the caller's
-    // order).  Otherwise positions [0, n) and res[position].
-    const uint32_t base = range ? range[2 * SUITE] : 0u;
-    const uint32_t lim = range ? range[2 * SUITE + 1] : n;
-    if (base + blockIdx.x * kPktPerWG >= lim) return;  // past this suite's bucket
-    auto res_of = [&](uint32_t p, const qpp_desc &dd) -> uint32_t { return range ? dd.rsv : p; };
-    __shared__ SuiteSmem<SUITE, WG> sm;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, wv);
+    if (W.empty_wg) return;  // past this suite's bucket
+    const uint32_t wb = W.b, we = W.e, planned = irange != nullptr;
+    __shared__ GcmSmem<WG> sm;
     // Thread-derived values are recomputed where they are used, from the
     // wave index (an SGPR) and a fresh lane id, instead of being kept live
     // across the packet loops: at 128 VGPRs anything live across the GCM step
     // loop is spilled to scratch (HBM traffic and latency).
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     auto tid_now = [&]() -> uint32_t { return (wv << 6) | lane_fresh(); };
-    auto pkt_of = [&](uint32_t t) -> uint32_t { return base + blockIdx.x * kPktPerWG + (t >> 2); };
+    auto pkt_of = [&](uint32_t t) -> uint32_t { return wb + ((t & 63) >> 2); };
+    // a lane's key slot, or kNoSlot (no packet, or a slot beyond the table)
+    auto slot_of = [&](const qpp_desc &d, uint32_t p) -> uint32_t {
+        return (p < we && d.slot < cap) ? d.slot : kNoSlot;
+    };
     QPP_PROBE_AT(0);
 
-    // Prologue: everything that depends only on the descriptor is requested
-    // at once (descriptor, then the header bytes that header protection needs),
-    // and the key slot is picked with one LDS min-reduction.  Each dependent
-    // global access costs microseconds at launch, when every CU issues at once.
-    uint32_t my_slot0 = kNoSlot;
+    // Prologue: descriptor, the workgroup's resident slots (its lowest
+    // distinct slots, one min-reduction each), their H^4 tables and the AES
+    // image into LDS.
     uint64_t in0 = ~0ull, out0 = ~0ull;
+    uint32_t my_slot = kNoSlot;
     {
         const uint32_t p = pkt_of(threadIdx.x);
-        const bool valid = p < lim;
         qpp_desc d = {};
-        if (valid) d = desc[p];
-#ifdef QPP_PROBE
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        QPP_PROBE_AT(10);
-#endif
-        if (threadIdx.x == 0) {
-            sm.cur_slot[0] = kNoSlot;
-            if constexpr (kGcm) sm.progress = 0;
-        }
-        if (valid) {
-            my_slot0 = d.slot;
+        if (p < we) d = desc[p];
+        my_slot = slot_of(d, p);
+        if (p < we) {
             in0 = d.in_off;
             out0 = d.out_off;
         }
-    }
-    // key material: speculate that the workgroup's packets use the slot of
-    // its first packet (host batches are grouped by slot) and stage it now
-    uint32_t staged = kNoSlot;
-    if constexpr (kGcm) {
-        const uint32_t spec = __builtin_amdgcn_readfirstlane(desc[base + blockIdx.x * kPktPerWG].slot);
-        if (spec < cap) {
-            stage_key<WG>(sm, slots, gtab, spec);
-            staged = spec;
+        if (threadIdx.x < kResident) sm.resident[threadIdx.x] = kNoSlot;
+        if (threadIdx.x == 0) {
+            sm.more = kNoSlot;
+            sm.progress = 0;
         }
-        load_te<WG>(sm.te);
     }
-#ifdef QPP_PROBE
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    QPP_PROBE_AT(11);
-    QPP_PROBE_AT(12);
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged key slot (LDS-DMA)
+    load_te<WG>(sm.te);
     __syncthreads();
-#ifdef QPP_PROBE
-    QPP_PROBE_AT(13);
-#endif
-    {
-        const uint32_t m = wave_min_u32(my_slot0);
-        if (__lane_id() == 0) atomicMin(&sm.cur_slot[0], m);
+    uint32_t lo = 0;
+    int nres = 0;
+    for (int r = 0; r <= kResident; ++r) {
+        const uint32_t m = wave_min_u32(my_slot >= lo ? my_slot : kNoSlot);
+        uint32_t *dst = r < kResident ? &sm.resident[r] : &sm.more;
+        if (__lane_id() == 0 && m != kNoSlot) atomicMin(dst, m);
+        __syncthreads();
+        const uint32_t got = __builtin_amdgcn_readfirstlane(*dst);
+        if (got == kNoSlot) break;
+        if (r < kResident) ++nres;
+        lo = got + 1;
+    }
+    // one slot: its four powers in buffers 0..3; two: H^1, H^4 of slot r in 2r, 2r + 1
+    for (int r = 0; r < nres; ++r) {
+        const uint32_t sl = __builtin_amdgcn_readfirstlane(sm.resident[r]);
+        if (slots[sl].suite != SUITE) continue;
+        if (nres == 1) {
+            for (int pw = 0; pw < 4; ++pw) stage_pow<WG>(sm, gtab, sl, pw, pw, 4 * pw);
+        } else {
+            stage_pow<WG>(sm, gtab, sl, 0, 2 * r, 8 * r);
+            stage_pow<WG>(sm, gtab, sl, 3, 2 * r + 1, 8 * r + 4);
+        }
     }
     // 32-bit buffer views based at this wave's lowest input / output offsets
     // (a wave's 16 packets must lie within 4 GiB of each other); wave-uniform
     const uint64_t bi = wave_min_u64(in0);
     const uint64_t bo = wave_min_u64(out0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident tables (LDS-DMA)
     __syncthreads();
     QPP_PROBE_AT(7);
 
-    // One iteration per distinct key slot in the workgroup, lowest first;
-    // cur_slot is double-buffered so the next minimum is reduced meanwhile.
-    // Slots are taken in increasing order, so a packet is done once its slot
-    // is <= the current one: no per-lane state crosses iterations.
-    for (int it = 0;; ++it) {
-        const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur_slot[it & 1]);
-        if (cur == kNoSlot) break;
-        if constexpr (kGcm) {
-            if (cur != staged) {  // the speculation missed, or a further slot
-                if (cur < cap) stage_key<WG>(sm, slots, gtab, cur);
-                staged = cur;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+    // The packets of one key slot `cur` among this wave's 16 (table buffer tb)
+    auto run_slot = [&](uint32_t cur, uint32_t tab_word) {
+        if (lane_fresh() == 0) {
+            sm.wslot[wv] = cur;
+            sm.wtab[wv] = tab_word;
         }
-        if (wv == 0 && lane_fresh() == 0) sm.cur_slot[(it + 1) & 1] = kNoSlot;
-        __syncthreads();
-        // GCM reads its key material from the staged LDS copy
-        const KeySlot *ks;
-        if constexpr (kGcm) ks = &sm.kslot;
-        else ks = slots + cur;
-        const uint32_t suite = cur < cap ? ks->suite : 0xffu;
-        const bool mine = suite == SUITE;
-        QPP_PROBE_AT(1);
-        // the descriptor is re-read each iteration (an L2 hit after the prologue)
+        const KeySlot *ks = slots + cur;
+        const uint32_t suite = ks->suite;
         const uint32_t t1 = tid_now(), p1 = pkt_of(t1);
-        const qpp_desc d = p1 < lim ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
-        const bool in_slot = d.slot == cur;
-        {
-            const uint32_t m = wave_min_u32(d.slot > cur ? d.slot : kNoSlot);
-            if (__lane_id() == 0 && m != kNoSlot) atomicMin(&sm.cur_slot[(it + 1) & 1], m);
-        }
-        if (in_slot && suite > QPP_CHACHA20_POLY1305 && (t1 & 3) == 0)
-            res[res_of(p1, d)] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};  // every suite's launch writes the same
-        if (in_slot && mine) {
-            const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
-            if constexpr (kGcm) {
-                const LdsTe T{sm.te, (t1 & 31) * 4};
-                Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
-                if (P.status == QPP_S_OK) {
-                    // plain keys for rounds 0-2 (counter cache) and NR, rotated between
-                    uint32_t rk[4 * (kNR + 1)];
+        const qpp_desc d = p1 < we ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
+        const bool mine = slot_of(d, p1) == cur;
+        // an empty slot: KeyUnavailableError (every suite's launch writes the same)
+        if (mine && suite > QPP_CHACHA20_POLY1305 && (t1 & 3) == 0)
+            res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+        if (!mine || suite != SUITE) return;  // the lambda's only early exit, at its top
+        const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
+        const LdsTe T{sm.te, (t1 & 31) * 4};
+        Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
+        if (P.status == QPP_S_OK) {
+            // plain keys for rounds 0-2 (counter cache) and NR, rotated between
+            uint32_t rk[4 * (kNR + 1)];
 #pragma unroll
-                    for (int i = 0; i < 4 * (kNR + 1); ++i)
-                        rk[i] = __builtin_amdgcn_readfirstlane(
-                            (i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
-                    const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
-                    const uint64_t rlen = (uint64_t)(P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN));
-                    const uint64_t wlen = (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN);
-                    if (ioff + rlen <= kBufBytes && ooff + wlen <= kBufBytes) {
-                        const Bufs B{
-                            __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
-                            __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
-                        uint8_t *scr = sm.scratch[t1 >> 2];
-                        const int hlen = P.hlen, clen = P.clen;
-                        const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 |
-                                               (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28;
-                        park(P, scr);
-                        *(u32x4 *)(scr + kScrHdr) = pre.h0;
-                        QPP_PROBE_AT(2);
-                        u32x4 got_tag;
-                        const u32x4 tag = gcm_packet<kNR, ENC>(
-                            P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], sm.gt,
-                            sm.te, B, P.src, (uint32_t)ioff,
-                            (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0],
-                            (kBalance && (!ENC || kBalanceEnc)) ? &sm.progress : nullptr, got_tag);
-                        QPP_PROBE_AT(4);
-                        // everything below is re-derived after the step loop
-                        const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
-                        const qpp_desc d2 = desc[p2];
-                        uint8_t *scr2 = sm.scratch[t2 >> 2];
-                        P = unpark(scr2, gin + d2.in_off, gout + d2.out_off);
-                        const LdsTe T2{sm.te, (t2 & 31) * 4};
-                        gcm_finish<ENC, SUITE>(P, ks, t2 & 3, scr2, T2, tag, got_tag);
-                    } else {
-                        P.status = QPP_S_LENGTH;  // workgroup spans more than 4 GiB
-                    }
-                }
-                const uint32_t t3 = tid_now(), p3 = pkt_of(t3);
-                write_result<ENC>(res, range ? desc[p3].rsv : p3, t3 & 3, P);
-                QPP_PROBE_AT(5);
+            for (int i = 0; i < 4 * (kNR + 1); ++i)
+                rk[i] = __builtin_amdgcn_readfirstlane((i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
+            const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
+            const uint64_t rlen = (uint64_t)(P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN));
+            const uint64_t wlen = (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN);
+            if (ioff + rlen <= kBufBytes && ooff + wlen <= kBufBytes) {
+                const Bufs B{
+                    __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
+                    __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
+                uint8_t *scr = sm.scratch[t1 >> 2];
+                const int hlen = P.hlen, clen = P.clen;
+                const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 |
+                                       (uint32_t)P.hp << 28;
+                park(P, scr);
+                *(u32x4 *)(scr + kScrHdr) = pre.h0;
+                QPP_PROBE_AT(2);
+                const GhashTabs G{&sm.h4[0][0], &sm.wtab[wv]};
+                u32x4 got_tag;
+                const u32x4 tag = gcm_packet<kNR, ENC>(
+                    P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
+                    (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0],
+                    (kBalance && (!ENC || kBalanceEnc)) ? &sm.progress : nullptr, got_tag);
+                QPP_PROBE_AT(4);
+                // everything below is re-derived after the step loop
+                const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
+                const qpp_desc d2 = desc[p2];
+                uint8_t *scr2 = sm.scratch[t2 >> 2];
+                P = unpark(scr2, gin + d2.in_off, gout + d2.out_off);
+                const LdsTe T2{sm.te, (t2 & 31) * 4};
+                const KeySlot *ks2 = slots + __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
+                gcm_finish<ENC, SUITE>(P, ks2, t2 & 3, scr2, T2, tag, got_tag);
             } else {
-                const ConstTe T;
-                Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
-                if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, t1 & 3, sm.scratch[t1 >> 2]);
-                write_result<ENC>(res, res_of(p1, d), t1 & 3, P);
+                P.status = QPP_S_LENGTH;  // the wave spans more than 4 GiB
             }
         }
+        const uint32_t t3 = tid_now(), p3 = pkt_of(t3);
+        write_result<ENC>(res, planned ? desc[p3].rsv : p3, t3 & 3, P);
+        QPP_PROBE_AT(5);
+    };
+
+    // Main phase: each wave on its own, slot by slot among its packets
+    // (lowest first; usually one), for the resident slots (those <= the last
+    // resident one).  A packet is done once its slot is <= the last run.
+    // (loop state lives in LDS: SGPRs are scarce across the step loop)
+    if (lane_fresh() == 0) sm.wlast[wv] = kNoSlot;
+    // bounded: a wave holds at most 16 distinct slots (watchdog against a
+    // logic error turning into a hung GPU)
+    #pragma unroll 1
+    for (int guard = 0; guard < 17; ++guard) {
+        const uint32_t more = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.more);
+        const uint32_t res_hi = more == kNoSlot ? 0xfffffffeu
+                                                : __builtin_amdgcn_readfirstlane(sm.resident[kResident - 1]);
+        const uint32_t last = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wlast[wv]);
+        const uint32_t t = tid_now(), p = pkt_of(t);
+        const qpp_desc d = p < we ? desc[p] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
+        const uint32_t s = slot_of(d, p);
+        const uint32_t cur = wave_min_u32((s <= res_hi && (last == kNoSlot || s > last)) ? s : kNoSlot);
+        if (cur == kNoSlot) break;
+        // table word: one resident slot -> all powers; else H^1 / H^4 of its pair
+        const bool single = __builtin_amdgcn_readfirstlane(sm.resident[1]) == kNoSlot;
+        const uint32_t tw = single ? (0u | 3u << 4 | kTabAll)
+                                   : (__builtin_amdgcn_readfirstlane(sm.resident[0]) == cur ? (0u | 1u << 4)
+                                                                                           : (2u | 3u << 4));
+        if (lane_fresh() == 0) sm.wlast[wv] = cur;
+        run_slot(cur, tw);
+    }
+    // packets whose slot lies beyond the table: KeyUnavailableError
+    {
+        const uint32_t t = tid_now(), p = pkt_of(t);
+        if (p < we && (t & 3) == 0) {
+            const qpp_desc d = desc[p];
+            if (d.slot >= cap) res[planned ? d.rsv : p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+        }
+    }
+    // Fallback phase, only when the workgroup holds more than kResident
+    // slots: the remaining ones one after the other through table buffer 0,
+    // the whole workgroup together.
+    if (__builtin_amdgcn_readfirstlane(sm.more) != kNoSlot) {
         __syncthreads();
+        if (threadIdx.x == 0) sm.cur[0] = __builtin_amdgcn_readfirstlane(sm.more);
+        __syncthreads();
+        for (int it = 0; it < WG / 4; ++it) {  // at most one per packet
+            const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur[it & 1]);
+            if (cur == kNoSlot) break;
+            if (slots[cur].suite == SUITE) {
+                stage_pow<WG>(sm, gtab, cur, 0, 0, 0);
+                stage_pow<WG>(sm, gtab, cur, 3, 1, 8);
+            }
+            if (wv == 0 && lane_fresh() == 0) sm.cur[(it + 1) & 1] = kNoSlot;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            {
+                const uint32_t t = tid_now(), p = pkt_of(t);
+                const qpp_desc d = p < we ? desc[p] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
+                const uint32_t s = slot_of(d, p);
+                const uint32_t m = wave_min_u32(s > cur ? s : kNoSlot);
+                if (__lane_id() == 0 && m != kNoSlot) atomicMin(&sm.cur[(it + 1) & 1], m);
+            }
+            run_slot(cur, 0u | 1u << 4);
+            __syncthreads();
+        }
     }
     QPP_PROBE_AT(6);
+}
+
+// ChaCha20-Poly1305: no tables, so every wave runs its packets slot by slot
+// on its own, with the keys read from the slot (scalar loads).
+template <bool ENC, int WG>
+__global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__restrict__ slots,
+                                                             uint32_t cap,
+                                                             const qpp_desc *__restrict__ desc,
+                                                             uint32_t n, const uint8_t *gin,
+                                                             uint8_t *gout,
+                                                             qpp_result *__restrict__ res,
+                                                             const uint32_t *__restrict__ items,
+                                                             const uint32_t *__restrict__ irange)
+{
+    constexpr int SUITE = QPP_CHACHA20_POLY1305;
+    const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    if (W.empty_wg) return;
+    const uint32_t lim = W.e, planned = irange != nullptr;
+    __shared__ ChachaSmem<WG> sm;
+    const uint32_t t1 = threadIdx.x, p1 = W.b + ((t1 & 63) >> 2);
+    if (p1 < lim && (t1 & 3) == 0) {
+        const qpp_desc d = desc[p1];
+        if (d.slot >= cap) res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+    }
+    // slot by slot among the wave's packets, lowest first (usually one); the
+    // descriptor is re-read each time rather than kept live (VGPRs)
+    // (bounded: a wave holds at most 16 distinct slots; structured, with no
+    // continue, so every lane reaches the loop's end each trip)
+    uint32_t last = kNoSlot;
+    #pragma unroll 1
+    for (int guard = 0; guard < 17; ++guard) {
+        const uint32_t s = p1 < lim ? desc[p1].slot : kNoSlot;
+        const uint32_t cur = wave_min_u32(s < cap && (last == kNoSlot || s > last) ? s : kNoSlot);
+        if (cur == kNoSlot) break;
+        const KeySlot *ks = slots + cur;
+        const uint32_t suite = ks->suite;
+        if (s == cur && suite > QPP_CHACHA20_POLY1305 && (t1 & 3) == 0) {
+            const qpp_desc d = desc[p1];
+            res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+        }
+        if (s == cur && suite == SUITE) {
+            const qpp_desc d = desc[p1];
+            const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
+            const ConstTe T;
+            Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
+            // lane-derived values from a fresh lane id: derived from t1 they
+            // would be hoisted out of the loop and held live across it
+            const uint32_t tf = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) << 6 | lane_fresh();
+            if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2]);
+            write_result<ENC>(res, planned ? desc[p1].rsv : p1, lane_fresh() & 3, P);
+        }
+        last = cur;
+    }
 }
 
 // Header-protection masks only (HeaderProtection_mask, _crypto.c:278-287).
@@ -1427,7 +1578,7 @@ static int wg_choice(const char *env, int dflt, bool chacha)
 
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                           const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream,
-                          const uint32_t *d_range = nullptr)
+                          const qpp_plan *plan = nullptr)
 {
     if (!kt || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
@@ -1436,37 +1587,53 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     // still gets one launch so every packet reports QPP_S_NO_KEY (planned,
     // the no-key bucket has its own kernel)
     uint32_t mask = keytab_suite_mask(kt);
-    if (!mask && !d_range) mask = 1u;
+    if (!mask && !plan) mask = 1u;
+    // planned: each suite's launch covers at most every wave item of the batch
+    const uint32_t *d_items = plan ? plan->d_items : nullptr, *d_irange = plan ? plan->d_irange : nullptr;
+    const uint32_t waves = plan ? qpp_internal_plan_max_items(n, kt->cap) : (n + 15) / 16;
     const int wg_gcm = wg_choice("QPP_WG_GCM", kGcmWG, false);
     const int wg_cc = enc ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
                           : wg_choice("QPP_WG_CHACHA_DEC", kChachaWGDec, true);
-#define QPP_LAUNCH_WG(SUITE, WGV)                                                              \
+#define QPP_LAUNCH_GCM_WG(SUITE, WGV)                                                          \
     do {                                                                                       \
-        const dim3 grid((n + WGV / 4 - 1) / (WGV / 4)), block(WGV);                            \
+        const dim3 grid((waves + WGV / 64 - 1) / (WGV / 64)), block(WGV);                      \
         if (enc)                                                                               \
-            hipLaunchKernelGGL((k_packets<SUITE, true, WGV>), grid, block, 0, s, kt->d_slots,  \
-                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_range);   \
+            hipLaunchKernelGGL((k_gcm<SUITE, true, WGV>), grid, block, 0, s, kt->d_slots,      \
+                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_items,    \
+                               d_irange);                                                      \
         else                                                                                   \
-            hipLaunchKernelGGL((k_packets<SUITE, false, WGV>), grid, block, 0, s, kt->d_slots, \
-                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_range);   \
+            hipLaunchKernelGGL((k_gcm<SUITE, false, WGV>), grid, block, 0, s, kt->d_slots,     \
+                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_items,    \
+                               d_irange);                                                      \
+    } while (0)
+#define QPP_LAUNCH_CHACHA_WG(WGV)                                                              \
+    do {                                                                                       \
+        const dim3 grid((waves + WGV / 64 - 1) / (WGV / 64)), block(WGV);                      \
+        if (enc)                                                                               \
+            hipLaunchKernelGGL((k_chacha<true, WGV>), grid, block, 0, s, kt->d_slots, kt->cap, \
+                               d_desc, n, d_in, d_out, d_res, d_items, d_irange);              \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_chacha<false, WGV>), grid, block, 0, s, kt->d_slots,         \
+                               kt->cap, d_desc, n, d_in, d_out, d_res, d_items, d_irange);     \
     } while (0)
 #define QPP_LAUNCH_GCM(SUITE)                                                                  \
     if (mask & (1u << SUITE)) {                                                                \
-        if (wg_gcm == 512) QPP_LAUNCH_WG(SUITE, 512);                                          \
-        else if (wg_gcm == 768) QPP_LAUNCH_WG(SUITE, 768);                                     \
-        else QPP_LAUNCH_WG(SUITE, 1024);                                                       \
+        if (wg_gcm == 512) QPP_LAUNCH_GCM_WG(SUITE, 512);                                      \
+        else if (wg_gcm == 768) QPP_LAUNCH_GCM_WG(SUITE, 768);                                 \
+        else QPP_LAUNCH_GCM_WG(SUITE, 1024);                                                   \
         HIPCHK(hipGetLastError());                                                             \
     }
     QPP_LAUNCH_GCM(QPP_AES_128_GCM)
     QPP_LAUNCH_GCM(QPP_AES_256_GCM)
     if (mask & (1u << QPP_CHACHA20_POLY1305)) {
-        if (wg_cc == 256) QPP_LAUNCH_WG(QPP_CHACHA20_POLY1305, 256);
-        else if (wg_cc == 1024) QPP_LAUNCH_WG(QPP_CHACHA20_POLY1305, 1024);
-        else QPP_LAUNCH_WG(QPP_CHACHA20_POLY1305, 512);
+        if (wg_cc == 256) QPP_LAUNCH_CHACHA_WG(256);
+        else if (wg_cc == 1024) QPP_LAUNCH_CHACHA_WG(1024);
+        else QPP_LAUNCH_CHACHA_WG(512);
         HIPCHK(hipGetLastError());
     }
 #undef QPP_LAUNCH_GCM
-#undef QPP_LAUNCH_WG
+#undef QPP_LAUNCH_GCM_WG
+#undef QPP_LAUNCH_CHACHA_WG
     return QPP_OK;
 }
 
@@ -1498,7 +1665,7 @@ static int launch_planned(bool enc, const qpp_keytab *kt, const qpp_plan *p, con
     hipStream_t s = (hipStream_t)stream;
     int rc = qpp_internal_plan_gather(p, d_desc, n, s);
     if (rc == QPP_OK)
-        rc = launch_packets(enc, kt, p->d_sorted, n, d_in, d_out, d_res, stream, p->d_range);
+        rc = launch_packets(enc, kt, p->d_sorted, n, d_in, d_out, d_res, stream, p);
     if (rc == QPP_OK) rc = qpp_internal_plan_nokey(p, d_res, s);
     return rc;
 }

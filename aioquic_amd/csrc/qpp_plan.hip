@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "qpp_internal.h"
 
@@ -53,6 +54,53 @@ __global__ void k_plan_ranges(const uint32_t *__restrict__ count, uint32_t *__re
         b += count[s];
         range[2 * s + 1] = b;
     }
+}
+
+constexpr uint32_t kItemPackets = 16;  // packets per wave in the packet kernels
+
+// flags[p] = 1 where sorted position p starts a wave item: its offset from the
+// start of its key's run (found by binary search in the sorted keys) is a
+// multiple of 16.
+__global__ __launch_bounds__(kPlanWG) void k_plan_heads(const uint32_t *__restrict__ skeys, uint32_t n,
+                                                        uint32_t *__restrict__ flags)
+{
+    const uint32_t p = blockIdx.x * kPlanWG + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t k = skeys[p];
+    uint32_t lo = 0, hi = p;  // first position holding k lies in [lo, hi]
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (skeys[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    flags[p] = ((p - lo) % kItemPackets) == 0 ? 1u : 0u;
+}
+
+// items[pos[p]] = p at every head; the last thread writes the sentinel and the
+// item count
+__global__ __launch_bounds__(kPlanWG) void k_plan_items(const uint32_t *__restrict__ flags,
+                                                        const uint32_t *__restrict__ pos, uint32_t n,
+                                                        uint32_t *__restrict__ items,
+                                                        uint32_t *__restrict__ total)
+{
+    const uint32_t p = blockIdx.x * kPlanWG + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t f = flags[p], i = pos[p];
+    if (f) items[i] = p;
+    if (p == n - 1) {
+        items[i + f] = n;
+        *total = i + f;
+    }
+}
+
+// range[8] (positions) -> irange[8] (items): a bucket starts on an item head
+__global__ void k_plan_iranges(const uint32_t *__restrict__ range, const uint32_t *__restrict__ pos,
+                               const uint32_t *__restrict__ total, uint32_t n,
+                               uint32_t *__restrict__ irange)
+{
+    if (threadIdx.x >= 8) return;
+    const uint32_t r = range[threadIdx.x];
+    irange[threadIdx.x] = r < n ? pos[r] : *total;
 }
 
 // sorted[p] = desc[idx[p]], with the caller's index in rsv
@@ -103,12 +151,17 @@ extern "C" int qpp_plan_create(uint32_t max_packets, qpp_plan **out)
     bool ok = hipMalloc(&p->d_keys[0], n * 4) == hipSuccess && hipMalloc(&p->d_keys[1], n * 4) == hipSuccess &&
               hipMalloc(&p->d_idx[0], n * 4) == hipSuccess && hipMalloc(&p->d_idx[1], n * 4) == hipSuccess &&
               hipMalloc(&p->d_sorted, n * sizeof(qpp_desc)) == hipSuccess &&
-              hipMalloc(&p->d_count, 16 * sizeof(uint32_t)) == hipSuccess;
+              hipMalloc(&p->d_flags, n * 4) == hipSuccess && hipMalloc(&p->d_pos, n * 4) == hipSuccess &&
+              hipMalloc(&p->d_items, (n + 1) * 4) == hipSuccess &&
+              hipMalloc(&p->d_count, 32 * sizeof(uint32_t)) == hipSuccess;
     if (ok) {
-        size_t tmp = 0;
+        size_t tmp = 0, tmp2 = 0;
         ok = rocprim::radix_sort_pairs(nullptr, tmp, p->d_keys[0], p->d_keys[1], p->d_idx[0], p->d_idx[1],
                                        max_packets, 0, 26) == hipSuccess &&
-             hipMalloc(&p->d_tmp, tmp ? tmp : 16) == hipSuccess;
+             rocprim::exclusive_scan(nullptr, tmp2, p->d_flags, p->d_pos, 0u, max_packets,
+                                     rocprim::plus<uint32_t>()) == hipSuccess;
+        if (tmp2 > tmp) tmp = tmp2;
+        ok = ok && hipMalloc(&p->d_tmp, tmp ? tmp : 16) == hipSuccess;
         p->tmp_bytes = tmp;
     }
     if (!ok) {
@@ -117,6 +170,7 @@ extern "C" int qpp_plan_create(uint32_t max_packets, qpp_plan **out)
         return QPP_E_NOMEM;
     }
     p->d_range = p->d_count + 8;
+    p->d_irange = p->d_count + 16;
     *out = p;
     return QPP_OK;
 }
@@ -130,6 +184,9 @@ extern "C" void qpp_plan_destroy(qpp_plan *p)
     }
     if (p->d_sorted) (void)hipFree(p->d_sorted);
     if (p->d_count) (void)hipFree(p->d_count);
+    if (p->d_flags) (void)hipFree(p->d_flags);
+    if (p->d_pos) (void)hipFree(p->d_pos);
+    if (p->d_items) (void)hipFree(p->d_items);
     if (p->d_tmp) (void)hipFree(p->d_tmp);
     free(p);
 }
@@ -138,17 +195,27 @@ int qpp_internal_plan_build(qpp_plan *p, const KeySlot *d_slots, uint32_t cap, c
                             uint32_t n, hipStream_t s)
 {
     if (n > p->cap) return QPP_E_ARG;
-    if (hipMemsetAsync(p->d_count, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return QPP_E_HIP;
+    if (hipMemsetAsync(p->d_count, 0, 32 * sizeof(uint32_t), s) != hipSuccess) return QPP_E_HIP;
     const int sb = bits_for(cap);
+    const dim3 grid((n + kPlanWG - 1) / kPlanWG);
     if (n) {
-        hipLaunchKernelGGL(k_plan_keys, dim3((n + kPlanWG - 1) / kPlanWG), dim3(kPlanWG), 0, s, d_slots, cap,
-                           d_desc, n, sb, p->d_keys[0], p->d_idx[0], p->d_count);
+        hipLaunchKernelGGL(k_plan_keys, grid, dim3(kPlanWG), 0, s, d_slots, cap, d_desc, n, sb, p->d_keys[0],
+                           p->d_idx[0], p->d_count);
         size_t tmp = p->tmp_bytes;
         if (rocprim::radix_sort_pairs(p->d_tmp, tmp, p->d_keys[0], p->d_keys[1], p->d_idx[0], p->d_idx[1], n,
                                       0, sb + 2, s) != hipSuccess)
             return QPP_E_HIP;
+        hipLaunchKernelGGL(k_plan_heads, grid, dim3(kPlanWG), 0, s, p->d_keys[1], n, p->d_flags);
+        tmp = p->tmp_bytes;
+        if (rocprim::exclusive_scan(p->d_tmp, tmp, p->d_flags, p->d_pos, 0u, n, rocprim::plus<uint32_t>(),
+                                    s) != hipSuccess)
+            return QPP_E_HIP;
+        hipLaunchKernelGGL(k_plan_items, grid, dim3(kPlanWG), 0, s, p->d_flags, p->d_pos, n, p->d_items,
+                           p->d_count + 24);
     }
     hipLaunchKernelGGL(k_plan_ranges, dim3(1), dim3(64), 0, s, p->d_count, p->d_range);
+    if (n) hipLaunchKernelGGL(k_plan_iranges, dim3(1), dim3(64), 0, s, p->d_range, p->d_pos, p->d_count + 24, n,
+                              p->d_irange);
     if (hipGetLastError() != hipSuccess) return QPP_E_HIP;
     p->n_built = n;
     return QPP_OK;
@@ -161,6 +228,14 @@ int qpp_internal_plan_gather(const qpp_plan *p, const qpp_desc *d_desc, uint32_t
     hipLaunchKernelGGL(k_plan_gather, dim3((n + kPlanWG - 1) / kPlanWG), dim3(kPlanWG), 0, s, d_desc,
                        p->d_idx[1], n, p->d_sorted);
     return hipGetLastError() == hipSuccess ? QPP_OK : QPP_E_HIP;
+}
+
+uint32_t qpp_internal_plan_max_items(uint32_t n, uint32_t cap)
+{
+    // every key run adds at most one partial item; runs <= distinct slots
+    // + the no-key bucket
+    const uint64_t m = (uint64_t)(n + kItemPackets - 1) / kItemPackets + (n < cap ? n : cap) + 1;
+    return (uint32_t)(m < n ? m : n);
 }
 
 int qpp_internal_plan_nokey(const qpp_plan *p, qpp_result *d_res, hipStream_t s)

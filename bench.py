@@ -62,6 +62,10 @@ def parse():
                     help="untimed steps first (the GPU clock needs ~20 ms of work to ramp)")
     ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
+    ap.add_argument("--order", choices=("grouped", "round_robin", "random"), default=None,
+                    help="override the config's arrival order (non-grouped orders are bucketed)")
+    ap.add_argument("--layout", choices=("arrival", "by_key"), default="arrival",
+                    help="study knob: by_key stores each key's packets contiguously")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-all-cores", type=int, default=1,
@@ -317,7 +321,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.order:
+        cfg["order"] = args.order
+        cfg["name"] += f" [{args.order} order]"
     n = args.packets or cfg["n"]
     from aioquic_amd.bench_data import make_workload
     from aioquic_amd.shard import shard_range
@@ -327,7 +334,9 @@ def main():
     seed = 0x9001 + (int(args.config) if args.config.isdigit() else 0)
     w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=seed,
                       version=cfg["version"], mixed=cfg.get("mixed"), first_packet=first,
-                      order=cfg.get("order", "grouped"))
+                      order=cfg.get("order", "grouped"), layout=args.layout)
+    if args.layout != "arrival":
+        cfg["name"] += f" [{args.layout} layout]"
     bucketed = cfg.get("order", "grouped") != "grouped"
     # the CPU baselines run before anything touches the GPU (they fork); at
     # N > 1 rank 0 times them while the other ranks wait at the first barrier

@@ -113,6 +113,41 @@ def test_planned_equals_unplanned_and_oracle(oracle):
         assert back_p[o : o + len(headers[i]) + len(payloads[i])].tobytes() == headers[i] + payloads[i]
 
 
+def test_wave_items_ragged_runs(oracle):
+    """Key runs of 1, 15, 16, 17, 31, 33, 64, 255 and 257 packets (the plan's
+    wave items split them at 16), all suites, shuffled arrival: planned ==
+    unplanned == oracle for every packet."""
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import PacketEngine, layout_packets
+
+    rng = np.random.default_rng(0x17E5)
+    runs = [1, 15, 16, 17, 31, 33, 64, 255, 257]
+    n_slots = 3 * len(runs)
+    recs = _keys(rng, n_slots)
+    eng = PacketEngine(n_slots)
+    eng.set_key_records(recs)
+    slots = np.concatenate([np.full(runs[s % len(runs)], s) for s in range(n_slots)])
+    rng.shuffle(slots)
+    n = len(slots)
+    headers, payloads, pns = [], [], []
+    for i in range(n):
+        pn = int(rng.integers(0, 1 << 20))
+        headers.append(short_header(rng.bytes(8), pn, 2, 0))
+        payloads.append(rng.bytes(int(rng.integers(20, 300))))
+        pns.append(pn)
+    inbuf, desc, size = layout_packets(headers, payloads, pns, [int(x) for x in slots])
+    out_u, res_u = _run(eng, "protect", desc, n, inbuf, size, False)
+    out_p, res_p = _run(eng, "protect", desc, n, inbuf, size, True)
+    assert (res_p["status"] == L.S_OK).all()
+    assert res_p.tobytes() == res_u.tobytes()
+    assert np.array_equal(out_p, out_u)
+    o_out, o_res = oracle.protect_batch(recs, desc, inbuf, size)
+    assert np.array_equal(o_res["out_len"], res_p["out_len"])
+    for i in range(n):
+        o, m = int(desc[i]["out_off"]), int(res_p[i]["out_len"])
+        assert np.array_equal(out_p[o : o + m], o_out[o : o + m]), i
+
+
 def _full_size(cfg, n, n_keys, seed, oracle):
     """Full-size random-arrival batch on device tensors, bucketed in the
     product: every tag verifies, the round trip is exact, decoded packet
