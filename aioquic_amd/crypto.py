@@ -1,20 +1,26 @@
-"""Packet protection with aioquic's API, executed on the GPU.
+"""QUIC packet protection contexts whose packet work runs on the GPU.
 
-Mirrors aioquic src/aioquic/quic/crypto.py (CIPHER_SUITES :12-16, salts :18-19,
-KeyUnavailableError :30, derive_key_iv_hp :34-56, CryptoContext :59-154,
-apply_key_phase / next_key_phase :148-168, CryptoPair :171-246) so it can
-replace that module under the QUIC connection machinery.
+Public surface = aioquic's ``quic/crypto.py`` (suite table :12-16, initial
+salts :18-19, ``KeyUnavailableError`` :30, ``derive_key_iv_hp`` :34-56,
+``CryptoContext`` :59-145, ``apply_key_phase`` / ``next_key_phase``
+:148-168, ``CryptoPair`` :171-246), so the connection code can import this
+module in its place.  The design underneath differs:
 
-CryptoContext keeps the reference's ``aead`` / ``hp`` attributes, but
-encrypt_packet / decrypt_packet run the FUSED device path (one launch does
-AEAD + header protection + packet-number decode), through a per-context
-two-slot key table: slot 0 = (aead, hp, key_phase), slot 1 = the transient
-next-phase key tried when a short header's key-phase bit flips
-(crypto.py:91-96).
+* A context owns a two-slot device key table (``_PhaseSlots``).  Slot 0 is
+  its current (AEAD key/IV, HP key, key phase); slot 1 is the next-phase
+  candidate, installed when the device reports a flipped key-phase bit
+  (``S_KEY_PHASE``; the reference tries ``next_key_phase`` at :91-96).
+* ``encrypt_packet`` / ``decrypt_packet`` are one fused device call each:
+  AEAD, header protection and packet-number recovery together, instead of
+  the reference's ``aead`` call followed by an ``hp`` call.
+* The ``aead`` / ``hp`` attributes stay the ``_crypto`` objects the
+  reference exposes; the slots are filled from their key material.
 """
 
-import binascii
-from typing import Callable, Optional
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, Optional, Tuple
 
 import numpy as np
 
@@ -23,271 +29,250 @@ from ._crypto import AEAD, CryptoError, HeaderProtection, KeyTable, protect_host
 from .packet import QuicProtocolVersion, decode_packet_number, is_long_header  # noqa: F401
 from .tls import CipherSuite, cipher_suite_hash, hkdf_expand_label, hkdf_extract
 
-CIPHER_SUITES = {
-    CipherSuite.AES_128_GCM_SHA256: (b"aes-128-ecb", b"aes-128-gcm"),
-    CipherSuite.AES_256_GCM_SHA384: (b"aes-256-ecb", b"aes-256-gcm"),
-    CipherSuite.CHACHA20_POLY1305_SHA256: (b"chacha20", b"chacha20-poly1305"),
+
+@dataclass(frozen=True)
+class _Suite:
+    hp_name: bytes
+    aead_name: bytes
+    key_len: int
+
+
+_SUITES: Dict[CipherSuite, _Suite] = {
+    CipherSuite.AES_128_GCM_SHA256: _Suite(b"aes-128-ecb", b"aes-128-gcm", 16),
+    CipherSuite.AES_256_GCM_SHA384: _Suite(b"aes-256-ecb", b"aes-256-gcm", 32),
+    CipherSuite.CHACHA20_POLY1305_SHA256: _Suite(b"chacha20", b"chacha20-poly1305", 32),
 }
+# (hp cipher, aead cipher) per suite, as the reference publishes it
+CIPHER_SUITES = {cs: (s.hp_name, s.aead_name) for cs, s in _SUITES.items()}
+
 INITIAL_CIPHER_SUITE = CipherSuite.AES_128_GCM_SHA256
-INITIAL_SALT_VERSION_1 = binascii.unhexlify("38762cf7f55934b34d179ae6a4c80cadccbb7f0a")
-INITIAL_SALT_VERSION_2 = binascii.unhexlify("0dede3def700a6db819381be6e269dcbf9bd2ed9")
+INITIAL_SALT_VERSION_1 = bytes.fromhex("38762cf7f55934b34d179ae6a4c80cadccbb7f0a")  # RFC 9001 5.2
+INITIAL_SALT_VERSION_2 = bytes.fromhex("0dede3def700a6db819381be6e269dcbf9bd2ed9")  # RFC 9369 3.3.1
 SAMPLE_SIZE = 16
 
 Callback = Callable[[str], None]
 
 
 def NoCallback(trigger: str) -> None:
-    pass
+    """Default setup / teardown hook: does nothing."""
 
 
 class KeyUnavailableError(CryptoError):
-    pass
+    """No key installed for the packet (decrypt before setup)."""
 
 
-def derive_key_iv_hp(
-    *, cipher_suite: CipherSuite, secret: bytes, version: int
-) -> tuple[bytes, bytes, bytes]:
-    algorithm = cipher_suite_hash(cipher_suite)
-    if cipher_suite in [
-        CipherSuite.AES_256_GCM_SHA384,
-        CipherSuite.CHACHA20_POLY1305_SHA256,
-    ]:
-        key_size = 32
-    else:
-        key_size = 16
-    prefix = b"quicv2 " if version == QuicProtocolVersion.VERSION_2 else b"quic "
-    return (
-        hkdf_expand_label(algorithm, secret, prefix + b"key", b"", key_size),
-        hkdf_expand_label(algorithm, secret, prefix + b"iv", b"", 12),
-        hkdf_expand_label(algorithm, secret, prefix + b"hp", b"", key_size),
-    )
+def _label_prefix(version: int) -> bytes:
+    # RFC 9369 sec. 3.3.2: QUIC v2 renames the packet-protection labels
+    return b"quicv2 " if version == QuicProtocolVersion.VERSION_2 else b"quic "
 
 
-def _raise_for(status: int) -> None:
-    if status == L.S_DECRYPT:
-        raise CryptoError("Payload decryption failed")
+def derive_key_iv_hp(*, cipher_suite: CipherSuite, secret: bytes, version: int) -> Tuple[bytes, bytes, bytes]:
+    """(AEAD key, IV, HP key) of a traffic secret (RFC 9001 sec. 5.1)."""
+    hash_alg = cipher_suite_hash(cipher_suite)
+    klen = _SUITES[cipher_suite].key_len
+    pre = _label_prefix(version)
+    sizes = ((b"key", klen), (b"iv", 12), (b"hp", klen))
+    out = tuple(hkdf_expand_label(hash_alg, secret, pre + name, b"", size) for name, size in sizes)
+    return out  # type: ignore[return-value]
+
+
+def _status_error(status: int) -> CryptoError:
     if status == L.S_NO_KEY:
-        raise KeyUnavailableError("Decryption key is not available")
-    raise CryptoError("Invalid payload length")
+        return KeyUnavailableError("Decryption key is not available")
+    if status == L.S_DECRYPT:
+        return CryptoError("Payload decryption failed")
+    return CryptoError("Invalid payload length")
 
 
-class _FusedSlots:
-    """Two device key slots holding (AEAD key/iv, HP key, key phase)."""
+def _one_desc(length: int, hdr_len: int, pn: int, slot: int) -> bytes:
+    rec = np.zeros(1, dtype=L.DESC)
+    rec[0]["len"], rec[0]["hdr_len"], rec[0]["slot"] = length, hdr_len, slot
+    rec[0]["pn"] = pn & 0xFFFFFFFFFFFFFFFF
+    return rec.tobytes()
+
+
+class _PhaseSlots:
+    """Device key table of one context: slot 0 = current keys, slot 1 = the
+    next key phase's.  A slot is rewritten only when the objects bound to it
+    change (identity of the AEAD / HP objects and the phase bit)."""
+
+    __slots__ = ("table", "_bound")
 
     def __init__(self) -> None:
         self.table = KeyTable(2)
-        self.ident = [None, None]
+        self._bound: list = [None, None]
 
-    def bind(self, slot: int, aead: AEAD, hp: HeaderProtection, key_phase: int) -> None:
-        ident = (id(aead), id(hp), key_phase)
-        if self.ident[slot] == ident:
+    def ensure(self, slot: int, aead: AEAD, hp: HeaderProtection, phase: int) -> None:
+        held = self._bound[slot]
+        if held is not None and held[0] is aead and held[1] is hp and held[2] == phase:
             return
         suite, key, iv = aead._material()
-        _, hp_key = hp._material()
-        self.table.set(L.key_material(slot, suite, key, iv, hp_key, key_phase).tobytes())
-        # keep the objects alive so their ids stay unique while bound
-        self.ident[slot] = ident
-        setattr(self, f"_keep{slot}", (aead, hp))
+        hp_key = hp._material()[1]
+        self.table.set(L.key_material(slot, suite, key, iv, hp_key, phase).tobytes())
+        # holding the objects keeps the identity test sound
+        self._bound[slot] = (aead, hp, phase)
 
 
-def _desc(length: int, hdr_len: int, pn: int, slot: int, flags: int = 0) -> bytes:
-    d = np.zeros(1, dtype=L.DESC)
-    d["len"] = length
-    d["hdr_len"] = hdr_len
-    d["pn"] = pn & 0xFFFFFFFFFFFFFFFF
-    d["slot"] = slot
-    d["flags"] = flags
-    return d.tobytes()
+def _unprotect_once(table: KeyTable, packet: bytes, offset: int, expected: int, slot: int):
+    desc = _one_desc(len(packet), offset, expected, slot)
+    out, res = unprotect_host(table, desc, packet, len(packet))
+    return out, np.frombuffer(res, dtype=L.RESULT)[0]
 
 
 class CryptoContext:
-    def __init__(
-        self,
-        key_phase: int = 0,
-        setup_cb: Callback = NoCallback,
-        teardown_cb: Callback = NoCallback,
-    ) -> None:
-        self.aead: Optional[AEAD] = None
-        self.cipher_suite: Optional[CipherSuite] = None
-        self.hp: Optional[HeaderProtection] = None
-        self.key_phase = key_phase
-        self.secret: Optional[bytes] = None
+    """Keys of one direction at one encryption level."""
+
+    def __init__(self, key_phase: int = 0, setup_cb: Callback = NoCallback,
+                 teardown_cb: Callback = NoCallback) -> None:
+        self._setup_cb, self._teardown_cb = setup_cb, teardown_cb
+        self._slots: Optional[_PhaseSlots] = None
         self.version: Optional[int] = None
-        self._setup_cb = setup_cb
-        self._teardown_cb = teardown_cb
-        self._slots: Optional[_FusedSlots] = None
+        self._forget()
+        self.key_phase = key_phase
 
-    def _fused(self) -> _FusedSlots:
-        if self._slots is None:
-            self._slots = _FusedSlots()
-        return self._slots
+    def _forget(self) -> None:
+        # what teardown clears (the version stays, as in the reference)
+        self.aead: Optional[AEAD] = None
+        self.hp: Optional[HeaderProtection] = None
+        self.cipher_suite: Optional[CipherSuite] = None
+        self.secret: Optional[bytes] = None
 
-    def decrypt_packet(
-        self, packet: bytes, encrypted_offset: int, expected_packet_number: int
-    ) -> tuple[bytes, bytes, int, bool]:
-        if self.aead is None:
-            raise KeyUnavailableError("Decryption key is not available")
-        if encrypted_offset > L.MAX_HDR:
-            raise CryptoError("Invalid payload length")
-        slots = self._fused()
-        slots.bind(0, self.aead, self.hp, self.key_phase)
-        desc = _desc(len(packet), encrypted_offset, expected_packet_number, 0)
-        out, res = unprotect_host(slots.table, desc, packet, len(packet))
-        r = np.frombuffer(res, dtype=L.RESULT)[0]
-        crypto = self
-        if r["status"] == L.S_KEY_PHASE:
-            # detect key phase change (quic/crypto.py:91-96): the HP key stays
-            crypto = next_key_phase(self)
-            slots.bind(1, crypto.aead, self.hp, crypto.key_phase)
-            desc = _desc(len(packet), encrypted_offset, expected_packet_number, 1)
-            out, res = unprotect_host(slots.table, desc, packet, len(packet))
-            r = np.frombuffer(res, dtype=L.RESULT)[0]
-        if r["status"] != L.S_OK:
-            _raise_for(int(r["status"]))
-        hl, n = int(r["hdr_len"]), int(r["out_len"])
-        return out[:hl], out[hl:n], int(r["pn"]), crypto is not self
+    def setup(self, *, cipher_suite: CipherSuite, secret: bytes, version: int) -> None:
+        suite = _SUITES[cipher_suite]
+        key, iv, hp_key = derive_key_iv_hp(cipher_suite=cipher_suite, secret=secret, version=version)
+        self.cipher_suite, self.secret, self.version = cipher_suite, secret, version
+        self.aead = AEAD(suite.aead_name, key, iv)
+        self.hp = HeaderProtection(suite.hp_name, hp_key)
+        self._setup_cb("tls")
 
-    def encrypt_packet(
-        self, plain_header: bytes, plain_payload: bytes, packet_number: int
-    ) -> bytes:
-        assert self.is_valid(), "Encryption key is not available"
-        slots = self._fused()
-        slots.bind(0, self.aead, self.hp, self.key_phase)
-        desc = _desc(len(plain_payload), len(plain_header), packet_number, 0)
-        n = len(plain_header) + len(plain_payload) + L.TAG_LEN
-        out, res = protect_host(slots.table, desc, plain_header + plain_payload, n)
-        r = np.frombuffer(res, dtype=L.RESULT)[0]
-        if r["status"] != L.S_OK:
-            _raise_for(int(r["status"]))
-        return out
+    def teardown(self) -> None:
+        self._forget()
+        self._slots = None
+        self._teardown_cb("tls")
 
     def is_valid(self) -> bool:
         return self.aead is not None
 
-    def setup(self, *, cipher_suite: CipherSuite, secret: bytes, version: int) -> None:
-        hp_cipher_name, aead_cipher_name = CIPHER_SUITES[cipher_suite]
+    def _device(self) -> _PhaseSlots:
+        if self._slots is None:
+            self._slots = _PhaseSlots()
+        self._slots.ensure(0, self.aead, self.hp, self.key_phase)
+        return self._slots
 
-        key, iv, hp = derive_key_iv_hp(
-            cipher_suite=cipher_suite,
-            secret=secret,
-            version=version,
-        )
-        self.aead = AEAD(aead_cipher_name, key, iv)
-        self.cipher_suite = cipher_suite
-        self.hp = HeaderProtection(hp_cipher_name, hp)
-        self.secret = secret
-        self.version = version
+    def encrypt_packet(self, plain_header: bytes, plain_payload: bytes, packet_number: int) -> bytes:
+        """Header + protected payload + tag, header protection applied."""
+        assert self.is_valid(), "Encryption key is not available"
+        dev = self._device()
+        total = len(plain_header) + len(plain_payload) + L.TAG_LEN
+        desc = _one_desc(len(plain_payload), len(plain_header), packet_number, 0)
+        out, res = protect_host(dev.table, desc, plain_header + plain_payload, total)
+        status = int(np.frombuffer(res, dtype=L.RESULT)[0]["status"])
+        if status != L.S_OK:
+            raise _status_error(status)
+        return out
 
-        # trigger callback
-        self._setup_cb("tls")
-
-    def teardown(self) -> None:
-        self.aead = None
-        self.cipher_suite = None
-        self.hp = None
-        self.secret = None
-        self._slots = None
-
-        # trigger callback
-        self._teardown_cb("tls")
+    def decrypt_packet(self, packet: bytes, encrypted_offset: int,
+                       expected_packet_number: int) -> Tuple[bytes, bytes, int, bool]:
+        """(plain header, payload, packet number, key phase changed)."""
+        if not self.is_valid():
+            raise KeyUnavailableError("Decryption key is not available")
+        if encrypted_offset > L.MAX_HDR:
+            raise CryptoError("Invalid payload length")
+        dev = self._device()
+        out, r = _unprotect_once(dev.table, packet, encrypted_offset, expected_packet_number, 0)
+        rotated = False
+        if r["status"] == L.S_KEY_PHASE:
+            # the peer moved to the next phase: same HP key, next AEAD key
+            candidate = next_key_phase(self)
+            dev.ensure(1, candidate.aead, self.hp, candidate.key_phase)
+            out, r = _unprotect_once(dev.table, packet, encrypted_offset, expected_packet_number, 1)
+            rotated = True
+        if r["status"] != L.S_OK:
+            raise _status_error(int(r["status"]))
+        cut, end = int(r["hdr_len"]), int(r["out_len"])
+        return out[:cut], out[cut:end], int(r["pn"]), rotated
 
 
 def apply_key_phase(self: CryptoContext, crypto: CryptoContext, trigger: str) -> None:
-    self.aead = crypto.aead
-    self.key_phase = crypto.key_phase
-    self.secret = crypto.secret
+    """Adopt `crypto`'s AEAD key, phase and secret (the HP key is kept)."""
+    self.aead, self.key_phase, self.secret = crypto.aead, crypto.key_phase, crypto.secret
+    hook = self._setup_cb
+    hook(trigger)
 
-    # trigger callback
-    self._setup_cb(trigger)
+
+def _updated_secret(ctx: CryptoContext) -> bytes:
+    # RFC 9001 sec. 6.1: "quic ku" (kept for QUIC v2 too, RFC 9369 sec. 3.3.2)
+    hash_alg = cipher_suite_hash(ctx.cipher_suite)
+    return hkdf_expand_label(hash_alg, ctx.secret, b"quic ku", b"", hash_alg.digest_size)
 
 
 def next_key_phase(self: CryptoContext) -> CryptoContext:
-    algorithm = cipher_suite_hash(self.cipher_suite)
+    """A fresh context on the next key phase of `self`."""
+    nxt = CryptoContext(key_phase=1 - int(bool(self.key_phase)))
+    nxt.setup(cipher_suite=self.cipher_suite, secret=_updated_secret(self), version=self.version)
+    return nxt
 
-    crypto = CryptoContext(key_phase=int(not self.key_phase))
-    crypto.setup(
-        cipher_suite=self.cipher_suite,
-        secret=hkdf_expand_label(
-            algorithm, self.secret, b"quic ku", b"", algorithm.digest_size
-        ),
-        version=self.version,
-    )
-    return crypto
+
+# (receive label, send label) by role, RFC 9001 sec. 5.2
+_INITIAL_LABELS: Dict[bool, Tuple[bytes, bytes]] = {
+    True: (b"server in", b"client in"),
+    False: (b"client in", b"server in"),
+}
+
+
+def _initial_salt(version: int) -> bytes:
+    if version == QuicProtocolVersion.VERSION_2:
+        return INITIAL_SALT_VERSION_2
+    return INITIAL_SALT_VERSION_1
 
 
 class CryptoPair:
-    def __init__(
-        self,
-        recv_setup_cb: Callback = NoCallback,
-        recv_teardown_cb: Callback = NoCallback,
-        send_setup_cb: Callback = NoCallback,
-        send_teardown_cb: Callback = NoCallback,
-    ) -> None:
-        self.aead_tag_size = 16
+    """Receive and send contexts of one encryption level, with key updates."""
+
+    def __init__(self, recv_setup_cb: Callback = NoCallback, recv_teardown_cb: Callback = NoCallback,
+                 send_setup_cb: Callback = NoCallback, send_teardown_cb: Callback = NoCallback) -> None:
         self.recv = CryptoContext(setup_cb=recv_setup_cb, teardown_cb=recv_teardown_cb)
         self.send = CryptoContext(setup_cb=send_setup_cb, teardown_cb=send_teardown_cb)
+        self.aead_tag_size = L.TAG_LEN
         self._update_key_requested = False
 
-    def decrypt_packet(
-        self, packet: bytes, encrypted_offset: int, expected_packet_number: int
-    ) -> tuple[bytes, bytes, int]:
-        plain_header, payload, packet_number, update_key = self.recv.decrypt_packet(
-            packet, encrypted_offset, expected_packet_number
-        )
-        if update_key:
-            self._update_key("remote_update")
-        return plain_header, payload, packet_number
+    @property
+    def key_phase(self) -> int:
+        phase = self.recv.key_phase
+        return int(not phase) if self._update_key_requested else phase
 
-    def encrypt_packet(
-        self, plain_header: bytes, plain_payload: bytes, packet_number: int
-    ) -> bytes:
+    def update_key(self) -> None:
+        """Start a key update with the next packet sent."""
+        self._update_key_requested = True
+
+    def _update_key(self, trigger: str) -> None:
+        for ctx in (self.recv, self.send):
+            apply_key_phase(ctx, next_key_phase(ctx), trigger=trigger)
+        self._update_key_requested = False
+
+    def setup_initial(self, cid: bytes, is_client: bool, version: int) -> None:
+        hash_alg = cipher_suite_hash(INITIAL_CIPHER_SUITE)
+        root = hkdf_extract(hash_alg, _initial_salt(version), cid)
+        for ctx, label in zip((self.recv, self.send), _INITIAL_LABELS[is_client]):
+            ctx.setup(
+                cipher_suite=INITIAL_CIPHER_SUITE,
+                secret=hkdf_expand_label(hash_alg, root, label, b"", hash_alg.digest_size),
+                version=version,
+            )
+
+    def teardown(self) -> None:
+        for ctx in (self.recv, self.send):
+            ctx.teardown()
+
+    def encrypt_packet(self, plain_header: bytes, plain_payload: bytes, packet_number: int) -> bytes:
         if self._update_key_requested:
             self._update_key("local_update")
         return self.send.encrypt_packet(plain_header, plain_payload, packet_number)
 
-    def setup_initial(self, cid: bytes, is_client: bool, version: int) -> None:
-        if is_client:
-            recv_label, send_label = b"server in", b"client in"
-        else:
-            recv_label, send_label = b"client in", b"server in"
-
-        if version == QuicProtocolVersion.VERSION_2:
-            initial_salt = INITIAL_SALT_VERSION_2
-        else:
-            initial_salt = INITIAL_SALT_VERSION_1
-
-        algorithm = cipher_suite_hash(INITIAL_CIPHER_SUITE)
-        initial_secret = hkdf_extract(algorithm, initial_salt, cid)
-        self.recv.setup(
-            cipher_suite=INITIAL_CIPHER_SUITE,
-            secret=hkdf_expand_label(
-                algorithm, initial_secret, recv_label, b"", algorithm.digest_size
-            ),
-            version=version,
-        )
-        self.send.setup(
-            cipher_suite=INITIAL_CIPHER_SUITE,
-            secret=hkdf_expand_label(
-                algorithm, initial_secret, send_label, b"", algorithm.digest_size
-            ),
-            version=version,
-        )
-
-    def teardown(self) -> None:
-        self.recv.teardown()
-        self.send.teardown()
-
-    def update_key(self) -> None:
-        self._update_key_requested = True
-
-    @property
-    def key_phase(self) -> int:
-        if self._update_key_requested:
-            return int(not self.recv.key_phase)
-        else:
-            return self.recv.key_phase
-
-    def _update_key(self, trigger: str) -> None:
-        apply_key_phase(self.recv, next_key_phase(self.recv), trigger=trigger)
-        apply_key_phase(self.send, next_key_phase(self.send), trigger=trigger)
-        self._update_key_requested = False
+    def decrypt_packet(self, packet: bytes, encrypted_offset: int,
+                       expected_packet_number: int) -> Tuple[bytes, bytes, int]:
+        header, payload, pn, rotated = self.recv.decrypt_packet(packet, encrypted_offset,
+                                                                expected_packet_number)
+        if rotated:
+            self._update_key("remote_update")
+        return header, payload, pn
