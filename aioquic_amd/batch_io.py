@@ -32,13 +32,12 @@ step (quic/connection.py:905-947, CryptoPair.decrypt_packet, crypto.py:184-192).
 
 from __future__ import annotations
 
-from dataclasses import dataclass
 from typing import Optional, Union
 
 import numpy as np
 
 from . import layout as L
-from ._crypto import CryptoError, KeyTable, protect_host, unprotect_host
+from ._crypto import CryptoError, KeyTable, protect_list, unprotect_list
 from .crypto import CryptoContext, CryptoPair, KeyUnavailableError, next_key_phase
 from .packet import decode_packet_number
 
@@ -116,14 +115,27 @@ def _context_of(crypto) -> CryptoContext:
 # ------------------------------------------------------------------ send --
 
 
-@dataclass
-class _SendItem:
-    aead: object
-    hp: object
-    key_phase: int
-    header: bytes
-    payload: bytes
-    pn: int
+class _KeyRefs:
+    """Distinct (aead, hp, key_phase) triples of a batch, by identity, so a
+    batch resolves key slots once per connection rather than per packet."""
+
+    __slots__ = ("index", "triples")
+
+    def __init__(self) -> None:
+        self.index: dict = {}
+        self.triples: list = []
+
+    def ref(self, aead, hp, key_phase: int) -> int:
+        k = (id(aead), id(hp), key_phase)
+        r = self.index.get(k)
+        if r is None:
+            r = self.index[k] = len(self.triples)
+            self.triples.append((aead, hp, key_phase))
+        return r
+
+    def slots(self, table: KeySlots, refs: list) -> bytes:
+        per = np.asarray(table.assign(self.triples), dtype=np.uint32)
+        return per[np.asarray(refs, dtype=np.int64)].tobytes()
 
 
 class SendBatch:
@@ -131,10 +143,17 @@ class SendBatch:
 
     def __init__(self, slots: Optional[KeySlots] = None, capacity: int = 1024) -> None:
         self.slots = slots or KeySlots(capacity)
-        self._items: list[_SendItem] = []
+        self._reset()
+
+    def _reset(self) -> None:
+        self._keys = _KeyRefs()
+        self._refs: list = []
+        self._headers: list = []
+        self._payloads: list = []
+        self._pns: list = []
 
     def __len__(self) -> int:
-        return len(self._items)
+        return len(self._refs)
 
     def add(self, crypto: Union[CryptoPair, CryptoContext], plain_header: bytes,
             plain_payload: bytes, packet_number: int) -> int:
@@ -147,44 +166,30 @@ class SendBatch:
             crypto._update_key("local_update")
         ctx = _context_of(crypto)
         assert ctx.is_valid(), "Encryption key is not available"
-        self._items.append(_SendItem(ctx.aead, ctx.hp, ctx.key_phase, bytes(plain_header),
-                                     bytes(plain_payload), int(packet_number)))
-        return len(self._items) - 1
+        self._refs.append(self._keys.ref(ctx.aead, ctx.hp, ctx.key_phase))
+        self._headers.append(bytes(plain_header))
+        self._payloads.append(bytes(plain_payload))
+        self._pns.append(packet_number & 0xFFFFFFFFFFFFFFFF)
+        return len(self._refs) - 1
 
-    def flush(self) -> list[bytes]:
+    def flush(self) -> list:
         """Protect every queued packet in one launch; returns the wire bytes in
         add() order.  Raises CryptoError("Invalid payload length") for the
         first packet that the reference would reject."""
-        items, self._items = self._items, []
-        if not items:
+        keys, refs, headers, payloads, pns = self._keys, self._refs, self._headers, self._payloads, self._pns
+        self._reset()
+        if not refs:
             return []
-        n = len(items)
-        slots = self.slots.assign([(it.aead, it.hp, it.key_phase) for it in items])
-        hl = np.fromiter((len(it.header) for it in items), np.int64, n)
-        pl = np.fromiter((len(it.payload) for it in items), np.int64, n)
-        out_sz = hl + pl + L.TAG_LEN
-        offs = np.zeros(n, np.int64)
-        np.cumsum(out_sz[:-1], out=offs[1:])
-        desc = np.zeros(n, dtype=L.DESC)
-        desc["in_off"] = offs
-        desc["out_off"] = offs
-        desc["len"] = pl
-        desc["hdr_len"] = np.minimum(hl, 0xFFFF)
-        desc["pn"] = np.fromiter((it.pn & 0xFFFFFFFFFFFFFFFF for it in items), np.uint64, n)
-        desc["slot"] = slots
-        # each packet occupies its output-sized region of the input (spare tag room)
-        data = b"".join(it.header + it.payload + bytes(L.TAG_LEN) for it in items)
-        total = int(offs[-1] + out_sz[-1])
-        for i, it in enumerate(items):
-            if len(it.header) > L.MAX_HDR:
-                raise CryptoError("Invalid payload length")
-        out, res = protect_host(self.slots.table, desc.tobytes(), data, total)
-        r = np.frombuffer(res, dtype=L.RESULT)
-        bad = np.nonzero(r["status"] != L.S_OK)[0]
+        if max(map(len, headers)) > L.MAX_HDR:
+            raise CryptoError("Invalid payload length")
+        slots = keys.slots(self.slots, refs)
+        wires, res = protect_list(self.slots.table, slots, np.asarray(pns, np.uint64).tobytes(),
+                                  headers, payloads)
+        status = np.frombuffer(res, dtype=L.RESULT)["status"]
+        bad = np.flatnonzero(status != L.S_OK)
         if len(bad):
-            raise _raise_status(int(r["status"][bad[0]]))
-        mv = memoryview(out)
-        return [bytes(mv[o : o + s]) for o, s in zip(offs.tolist(), out_sz.tolist())]
+            raise _raise_status(int(status[bad[0]]))
+        return wires
 
 
 # --------------------------------------------------------------- receive --
@@ -197,15 +202,6 @@ class _Space:
 
     def __init__(self, v: int) -> None:
         self.expected_packet_number = v
-
-
-@dataclass
-class _RecvItem:
-    pair: CryptoPair
-    packet: bytes
-    pn_off: int
-    space: object
-    track: bool
 
 
 def _signed_trunc(pn: int, pn_len: int) -> int:
@@ -222,11 +218,15 @@ class ReceiveBatch:
 
     def __init__(self, slots: Optional[KeySlots] = None, capacity: int = 1024) -> None:
         self.slots = slots or KeySlots(capacity)
-        self._items: list[_RecvItem] = []
+        self._pairs: list = []
+        self._packets: list = []
+        self._offs: list = []
+        self._spaces: list = []
+        self._track: list = []
         self.launches = 0
 
     def __len__(self) -> int:
-        return len(self._items)
+        return len(self._pairs)
 
     def add(self, pair: CryptoPair, packet: bytes, encrypted_offset: int,
             expected_packet_number: Optional[int] = None, space=None) -> int:
@@ -236,124 +236,118 @@ class ReceiveBatch:
         if (expected_packet_number is None) == (space is None):
             raise ValueError("give exactly one of expected_packet_number / space")
         track = space is not None
-        sp = space if track else _Space(int(expected_packet_number))
-        self._items.append(_RecvItem(pair, bytes(packet), int(encrypted_offset), sp, track))
-        return len(self._items) - 1
+        self._pairs.append(pair)
+        self._packets.append(bytes(packet))
+        self._offs.append(int(encrypted_offset))
+        self._spaces.append(space if track else _Space(int(expected_packet_number)))
+        self._track.append(track)
+        return len(self._pairs) - 1
 
-    def _launch(self, idx, keys, expected):
-        """One unprotect launch over items idx with (aead, hp, key_phase) keys;
-        returns (out bytes, results, offsets)."""
-        items = [self._items[i] for i in idx]
-        n = len(items)
-        slots = self.slots.assign(keys)
-        lens = np.fromiter((len(it.packet) for it in items), np.int64, n)
-        offs = np.zeros(n, np.int64)
-        np.cumsum(lens[:-1], out=offs[1:])
-        desc = np.zeros(n, dtype=L.DESC)
-        desc["in_off"] = offs
-        desc["out_off"] = offs
-        desc["len"] = lens
-        desc["hdr_len"] = [min(it.pn_off, 0xFFFF) for it in items]
-        desc["pn"] = np.asarray([e & 0xFFFFFFFFFFFFFFFF for e in expected], dtype=np.uint64)
-        desc["slot"] = slots
-        data = b"".join(it.packet for it in items)
-        out, res = unprotect_host(self.slots.table, desc.tobytes(), data, len(data))
+    def _launch(self, idx: list, triples: list, expected: list):
+        """One unprotect launch over items idx with per-item (aead, hp,
+        key_phase); returns (list of (header, payload) | None, status list,
+        pn list, hdr_len list)."""
+        keys = _KeyRefs()
+        refs = [keys.ref(*t) for t in triples]
+        slots = keys.slots(self.slots, refs)
+        outs, res = unprotect_list(self.slots.table, slots,
+                                   np.asarray([e & 0xFFFFFFFFFFFFFFFF for e in expected], np.uint64).tobytes(),
+                                   [self._packets[i] for i in idx],
+                                   np.asarray([min(self._offs[i], 0xFFFF) for i in idx], np.uint32).tobytes())
         self.launches += 1
-        return out, np.frombuffer(res, dtype=L.RESULT), offs
+        r = np.frombuffer(res, dtype=L.RESULT)
+        return outs, r["status"].tolist(), r["pn"].tolist(), r["hdr_len"].tolist()
 
     def run(self) -> list:
-        items, n = self._items, len(self._items)
+        pairs, spaces, track, offs = self._pairs, self._spaces, self._track, self._offs
+        n = len(pairs)
         outcome: list = [None] * n
         todo = list(range(n))
+        # per item of the current round, by item index
+        r_out: list = [None] * n
+        r_st: list = [None] * n
+        r_pn: list = [0] * n
+        r_hl: list = [0] * n
+        exp_at: list = [0] * n
         while todo:
-            # items whose pair has no receive key fail up front (crypto.py:78-79)
-            launch = []
-            for i in todo:
-                if items[i].pair.recv.aead is None:
-                    continue
-                launch.append(i)
-            # snapshot of each pair's receive keys at launch time; _update_key
-            # mutates the context in place (apply_key_phase, crypto.py:148-154)
-            ctx = {i: items[i].pair.recv for i in launch}
-            cur = {i: (ctx[i].aead, ctx[i].hp, ctx[i].key_phase) for i in launch}
-            exp_at = {i: items[i].space.expected_packet_number for i in launch}
-            resA = {}
+            # items whose pair has no receive key fail up front (crypto.py:78-79);
+            # a pn offset beyond the header limit fails host-side (length)
+            launch = [i for i in todo if pairs[i].recv.aead is not None and offs[i] <= L.MAX_HDR]
+            keys = []
             for i in launch:
-                if items[i].pn_off > L.MAX_HDR:
-                    resA[i] = None  # Invalid payload length, host-side
-            run_a = [i for i in launch if i not in resA]
-            if run_a:
-                out, r, offs = self._launch(run_a, [cur[i] for i in run_a], [exp_at[i] for i in run_a])
-                for k, i in enumerate(run_a):
-                    resA[i] = (out, r[k], int(offs[k]))
+                rc = pairs[i].recv
+                keys.append((rc.aead, rc.hp, rc.key_phase))
+                exp_at[i] = spaces[i].expected_packet_number
+            flip = []
+            if launch:
+                outs, st, pn, hl = self._launch(launch, keys, [exp_at[i] for i in launch])
+                for k, i in enumerate(launch):
+                    r_out[i], r_st[i], r_pn[i], r_hl[i] = outs[k], st[k], pn[k], hl[k]
+                    if st[k] == L.S_KEY_PHASE:
+                        flip.append((i, keys[k]))
             # second launch: short-header packets whose key phase bit flipped,
             # on the next-phase key (same HP key), crypto.py:91-96
-            flip = [i for i in run_a if int(resA[i][1]["status"]) == L.S_KEY_PHASE]
-            nxt_ctx = {}
-            resB = {}
+            rolled_at = set()
             if flip:
-                keys = []
-                for i in flip:
-                    k = id(cur[i][0])
-                    if k not in nxt_ctx:
-                        nxt = next_key_phase(ctx[i])
-                        nxt_ctx[k] = (nxt.aead, ctx[i].hp, nxt.key_phase)
-                    keys.append(nxt_ctx[k])
-                out, r, offs = self._launch(flip, keys, [exp_at[i] for i in flip])
-                for k, i in enumerate(flip):
-                    resB[i] = (out, r[k], int(offs[k]))
-            # walk in order, applying each packet's effect on its pair
+                nxt_keys: dict = {}
+                triples = []
+                for i, cur in flip:
+                    k = id(cur[0])
+                    if k not in nxt_keys:
+                        nxt = next_key_phase(pairs[i].recv)
+                        nxt_keys[k] = (nxt.aead, cur[1], nxt.key_phase)
+                    triples.append(nxt_keys[k])
+                idx = [i for i, _ in flip]
+                outs, st, pn, hl = self._launch(idx, triples, [exp_at[i] for i in idx])
+                for k, i in enumerate(idx):
+                    r_out[i], r_st[i], r_pn[i], r_hl[i] = outs[k], st[k], pn[k], hl[k]
+                    rolled_at.add(i)
+            # walk in order, applying each packet's effect on its pair.  Keys
+            # only change here (a roll blocks its pair for the rest of the
+            # round), so every unblocked pair still has its launch-time keys.
             blocked: set = set()
             stale = []
             for i in todo:
-                it = items[i]
-                pid = id(it.pair)
-                if pid in blocked:
+                pair = pairs[i]
+                if blocked and id(pair) in blocked:
                     stale.append(i)
                     continue
-                if it.pair.recv.aead is None:
+                if pair.recv.aead is None:
                     outcome[i] = KeyUnavailableError("Decryption key is not available")
                     continue
-                rc = it.pair.recv
-                if i not in cur or (rc.aead, rc.hp, rc.key_phase) != cur[i]:
-                    blocked.add(pid)
-                    stale.append(i)
-                    continue
-                got = resA[i]
-                if got is None:
+                status = r_st[i]
+                if status is None:  # the offset check failed
                     outcome[i] = CryptoError("Invalid payload length")
                     continue
-                rolled = False
-                if int(got[1]["status"]) == L.S_KEY_PHASE:
-                    got = resB[i]
-                    rolled = True
-                out, r, off = got
-                st = int(r["status"])
-                exp_now = it.space.expected_packet_number
-                if exp_now != exp_at[i] and st != L.S_OK:
-                    # decoded under an expected number an earlier packet has
-                    # since raised: the packet number, hence the nonce, may
-                    # differ now, so a failure is not final -- relaunch
-                    blocked.add(pid)
-                    stale.append(i)
+                space = spaces[i]
+                exp_now = space.expected_packet_number
+                moved = exp_now != exp_at[i]
+                if status != L.S_OK:
+                    if moved:
+                        # decoded under an expected number an earlier packet
+                        # has since raised: the packet number, hence the
+                        # nonce, may differ now -- relaunch
+                        blocked.add(id(pair))
+                        stale.append(i)
+                    else:
+                        outcome[i] = _raise_status(status)
                     continue
-                if st == L.S_OK:
-                    hl, ln, pn = int(r["hdr_len"]), int(r["out_len"]), int(r["pn"])
-                    if exp_now != exp_at[i]:
-                        pn_len = hl - it.pn_off
-                        again = decode_packet_number(_signed_trunc(pn, pn_len), pn_len * 8, exp_now)
-                        if again != pn:  # decoded under a stale expected number
-                            blocked.add(pid)
-                            stale.append(i)
-                            continue
-                    outcome[i] = (bytes(out[off : off + hl]), bytes(out[off + hl : off + ln]), pn)
-                    if rolled:
-                        it.pair._update_key("remote_update")
-                        blocked.add(pid)
-                    if it.track and pn > it.space.expected_packet_number:
-                        it.space.expected_packet_number = pn + 1
-                else:
-                    outcome[i] = _raise_status(st)
+                pn = r_pn[i]
+                if moved:
+                    pn_len = r_hl[i] - offs[i]
+                    if decode_packet_number(_signed_trunc(pn, pn_len), pn_len * 8, exp_now) != pn:
+                        blocked.add(id(pair))  # decoded under a stale expected number
+                        stale.append(i)
+                        continue
+                out = r_out[i]
+                outcome[i] = (out[0], out[1], pn)
+                if i in rolled_at:
+                    pair._update_key("remote_update")
+                    blocked.add(id(pair))
+                if track[i] and pn > exp_now:
+                    space.expected_packet_number = pn + 1
+            for i in stale:
+                r_st[i] = None
             todo = stale
-        self._items = []
+        self._pairs, self._packets, self._offs, self._spaces, self._track = [], [], [], [], []
         return outcome

@@ -711,6 +711,133 @@ static PyObject *batch_into(PyObject *args, int enc)
 static PyObject *py_protect_into(PyObject *m, PyObject *args) { return batch_into(args, 1); }
 static PyObject *py_unprotect_into(PyObject *m, PyObject *args) { return batch_into(args, 0); }
 
+/* protect_list(table, slots_u32, pns_u64, headers, payloads) -> (wires, results)
+ * unprotect_list(table, slots_u32, expected_u64, packets, pn_offs_u32)
+ *     -> (list of (plain_header, payload) or None, results)
+ * The batched callers' form: the packets are copied straight from the bytes
+ * objects of the lists into the session's pinned staging buffer, and the
+ * outputs are cut straight from its pinned output buffer, one bytes object
+ * each; no intermediate joins or slices in Python. */
+static PyObject *batch_list(PyObject *args, int enc)
+{
+    PyObject *t, *items;
+    const char *slots, *nums, *extra = NULL;
+    Py_ssize_t slots_len, nums_len, extra_len = 0;
+    PyObject *payloads = NULL;
+    if (enc) {
+        if (!PyArg_ParseTuple(args, "Oy#y#O!O!", &t, &slots, &slots_len, &nums, &nums_len, &PyList_Type,
+                              &items, &PyList_Type, &payloads))
+            return NULL;
+    } else if (!PyArg_ParseTuple(args, "Oy#y#O!y#", &t, &slots, &slots_len, &nums, &nums_len, &PyList_Type,
+                                 &items, &extra, &extra_len)) {
+        return NULL;
+    }
+    qpp_keytab *kt = as_table(t);
+    if (!kt) return NULL;
+    const Py_ssize_t n = PyList_Size(items);
+    if (slots_len != 4 * n || nums_len != 8 * n || (enc ? PyList_Size(payloads) != n : extra_len != 4 * n)) {
+        PyErr_SetString(PyExc_ValueError, "per-packet arrays do not match the packet list");
+        return NULL;
+    }
+    if (n > 0x7fffffff) {
+        PyErr_SetString(PyExc_ValueError, "batch too large");
+        return NULL;
+    }
+    /* first pass: sizes (and the type check of every item) */
+    size_t total = 0;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        char *b;
+        Py_ssize_t l1, l2 = 0;
+        if (PyBytes_AsStringAndSize(PyList_GetItem(items, i), &b, &l1) < 0) return NULL;
+        if (enc && PyBytes_AsStringAndSize(PyList_GetItem(payloads, i), &b, &l2) < 0) return NULL;
+        total += (size_t)l1 + (size_t)l2 + (enc ? QPP_TAG_LEN : 0);
+    }
+    qpp_session *s = session();
+    if (!s) return NULL;
+    PyObject *res = PyBytes_FromStringAndSize(NULL, n * (Py_ssize_t)sizeof(qpp_result));
+    qpp_desc *desc = (qpp_desc *)calloc(n ? (size_t)n : 1, sizeof(qpp_desc));
+    uint8_t *hin = NULL, *hout = NULL;
+    PyObject *ret = NULL, *outs = NULL;
+    if (!res || !desc) {
+        PyErr_NoMemory();
+        goto done;
+    }
+    if (n == 0) {
+        outs = PyList_New(0);
+        goto pack;
+    }
+    if (check_rc(qpp_session_stage(s, total ? total : 1, (uint32_t)n, &hin, &hout)) < 0) goto done;
+    {
+        const uint32_t *sl = (const uint32_t *)slots;
+        size_t off = 0;
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            char *b1, *b2 = NULL;
+            Py_ssize_t l1, l2 = 0;
+            (void)PyBytes_AsStringAndSize(PyList_GetItem(items, i), &b1, &l1);
+            if (enc) (void)PyBytes_AsStringAndSize(PyList_GetItem(payloads, i), &b2, &l2);
+            qpp_desc *d = &desc[i];
+            d->in_off = d->out_off = off;
+            uint64_t num;
+            memcpy(&num, nums + 8 * i, 8);
+            d->pn = num;
+            d->slot = sl[i];
+            memcpy(hin + off, b1, (size_t)l1);
+            if (enc) {
+                /* a header the 16-bit field cannot carry is rejected below */
+                d->hdr_len = l1 > 0xffff ? 0xffff : (uint16_t)l1;
+                d->len = (uint32_t)l2;
+                memcpy(hin + off + l1, b2, (size_t)l2);
+                off += (size_t)l1 + (size_t)l2 + QPP_TAG_LEN;
+            } else {
+                uint32_t po;
+                memcpy(&po, extra + 4 * i, 4);
+                d->hdr_len = po > 0xffff ? 0xffff : (uint16_t)po;
+                d->len = (uint32_t)l1;
+                off += (size_t)l1;
+            }
+        }
+    }
+    if (host_call(enc, kt, desc, (uint32_t)n, hin, total, hout, total, PyBytes_AsString(res)) < 0) goto done;
+    outs = PyList_New(n);
+    if (!outs) goto done;
+    {
+        const qpp_result *r = (const qpp_result *)PyBytes_AsString(res);
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            const uint8_t *o = hout + desc[i].out_off;
+            PyObject *item;
+            if (enc) {
+                item = PyBytes_FromStringAndSize((const char *)o, (Py_ssize_t)desc[i].hdr_len + desc[i].len +
+                                                                      QPP_TAG_LEN);
+            } else if (r[i].status == QPP_S_OK) {
+                PyObject *h = PyBytes_FromStringAndSize((const char *)o, r[i].hdr_len);
+                PyObject *p = PyBytes_FromStringAndSize((const char *)o + r[i].hdr_len,
+                                                        (Py_ssize_t)r[i].out_len - r[i].hdr_len);
+                item = (h && p) ? PyTuple_Pack(2, h, p) : NULL;
+                Py_XDECREF(h);
+                Py_XDECREF(p);
+            } else {
+                Py_INCREF(Py_None);
+                item = Py_None;
+            }
+            if (!item) {
+                Py_CLEAR(outs);
+                goto done;
+            }
+            PyList_SetItem(outs, i, item); /* steals */
+        }
+    }
+pack:
+    if (outs) ret = PyTuple_Pack(2, outs, res);
+done:
+    Py_XDECREF(outs);
+    Py_XDECREF(res);
+    free(desc);
+    return ret;
+}
+
+static PyObject *py_protect_list(PyObject *m, PyObject *args) { return batch_list(args, 1); }
+static PyObject *py_unprotect_list(PyObject *m, PyObject *args) { return batch_list(args, 0); }
+
 static PyObject *py_hp_mask_host(PyObject *m, PyObject *args)
 {
     PyObject *t;
@@ -756,6 +883,10 @@ static PyMethodDef module_methods[] = {
     {"unprotect_host", py_unprotect_host, METH_VARARGS, "unprotect_host(table, desc, data, out_len) -> (out, results)"},
     {"protect_into", py_protect_into, METH_VARARGS, "protect_into(table, desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
     {"unprotect_into", py_unprotect_into, METH_VARARGS, "unprotect_into(table, desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
+    {"protect_list", py_protect_list, METH_VARARGS,
+     "protect_list(table, slots_u32, pns_u64, headers, payloads) -> (wires, results)"},
+    {"unprotect_list", py_unprotect_list, METH_VARARGS,
+     "unprotect_list(table, slots_u32, expected_u64, packets, pn_offs_u32) -> (list of (header, payload) | None, results)"},
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},

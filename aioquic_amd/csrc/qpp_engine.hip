@@ -1905,7 +1905,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         }
         if (hi > in_len) hi = in_len;
         if (lo < hi) {
-            par_memcpy(s->h_in + lo, in + lo, hi - lo);
+            if (in != s->h_in) par_memcpy(s->h_in + lo, in + lo, hi - lo);
             HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice,
                                   s->s_in));
         }
@@ -1928,14 +1928,16 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
                 break;
             }
             const int d = next_out++;
-            if (olo[d + 1] > olo[d]) par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d]);
+            if (olo[d + 1] > olo[d] && out != s->h_out)
+                par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d]);
         }
     }
     if (rc != QPP_OK) return rc;
     HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->s_out));
     for (int c = next_out; c < chunks; ++c) {
         HIPCHK(hipEventSynchronize(s->ev_out[c]));
-        if (olo[c + 1] > olo[c]) par_memcpy(out + olo[c], s->h_out + olo[c], olo[c + 1] - olo[c]);
+        if (olo[c + 1] > olo[c] && out != s->h_out)
+            par_memcpy(out + olo[c], s->h_out + olo[c], olo[c + 1] - olo[c]);
     }
     HIPCHK(hipStreamSynchronize(s->s_out));
     memcpy(res, hr, (size_t)n * sizeof(qpp_result));
@@ -1981,7 +1983,7 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     memcpy(hd, desc, (size_t)n * sizeof(qpp_desc));
     reject_out_of_bounds(enc, hd, n, in_len, out_len);
-    if (in_len) memcpy(s->h_in, in, in_len);
+    if (in_len && in != s->h_in) memcpy(s->h_in, in, in_len);  // staged by the caller already?
     HIPCHK(hipMemcpyAsync(dd, hd, (size_t)n * sizeof(qpp_desc), hipMemcpyHostToDevice, s->stream));
     if (in_len) HIPCHK(hipMemcpyAsync(s->d_in, s->h_in, in_len, hipMemcpyHostToDevice, s->stream));
     // bytes the kernel does not write (gaps, failed packets) come back as zeros
@@ -1991,7 +1993,7 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
     if (out_len) HIPCHK(hipMemcpyAsync(s->h_out, s->d_out, out_len, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
-    if (out_len) memcpy(out, s->h_out, out_len);
+    if (out_len && out != s->h_out) memcpy(out, s->h_out, out_len);
     memcpy(res, hr, (size_t)n * sizeof(qpp_result));
     return QPP_OK;
 }
@@ -2008,6 +2010,16 @@ int qpp_session_unprotect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *
                           size_t out_len, qpp_result *res)
 {
     return session_drain_on_error(s, session_run(false, s, kt, desc, n, in, in_len, out, out_len, res));
+}
+
+int qpp_session_stage(qpp_session *s, size_t bytes, uint32_t n, uint8_t **h_in, uint8_t **h_out)
+{
+    if (!s || !h_in || !h_out) return QPP_E_ARG;
+    const int rc = session_reserve(s, bytes, n);
+    if (rc != QPP_OK) return rc;
+    *h_in = s->h_in;
+    *h_out = s->h_out;
+    return QPP_OK;
 }
 
 int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *slots,

@@ -9,7 +9,16 @@ CipherSuite :294-298, CIPHER_SUITES hash map :1108-1112, cipher_suite_hash
 import hashlib
 import hmac
 import struct
-from enum import IntEnum
+from enum import Enum, IntEnum
+
+
+class Epoch(Enum):
+    """Encryption levels (tls.py:129-133)."""
+
+    INITIAL = 0
+    ZERO_RTT = 1
+    HANDSHAKE = 2
+    ONE_RTT = 3
 
 
 class CipherSuite(IntEnum):

@@ -208,6 +208,12 @@ int qpp_session_unprotect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *
                           size_t out_len, qpp_result *res);
 int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *slots,
                         const uint8_t *samples, uint32_t n, uint8_t *masks);
+/* The session's own pinned staging buffers, sized for at least `bytes` of
+ * input and of output and n packets; valid until the next call on the
+ * session.  A caller that assembles its input straight into *h_in and passes
+ * h_in / h_out as `in` / `out` to qpp_session_protect / _unprotect saves both
+ * staging copies (the batched Python callers do). */
+int qpp_session_stage(qpp_session *s, size_t bytes, uint32_t n, uint8_t **h_in, uint8_t **h_out);
 int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material *km,
                          uint32_t n);
 
