@@ -377,20 +377,41 @@ struct Bufs {
 
 // --------------------------------------------------------------- AES-GCM --
 
-// Phase timestamps per wave (tools/probe.hip builds with -DQPP_PROBE):
-// 100 MHz s_memrealtime, written by the wave's first active lane.
+// Phase times per wave (tools/probe.hip builds with -DQPP_PROBE): each mark
+// adds the 100 MHz s_memrealtime ticks since the wave's previous mark to
+// g_probe[wave][i] (slot kProbeItems counts items; kProbeStart / kProbeEnd
+// hold the wave's first and last timestamps).
 #ifdef QPP_PROBE
-constexpr int kProbeSlots = 16;
-constexpr uint32_t kProbeWaves = 8192;  // waves recorded (tools/probe.hip caps n)
+constexpr int kProbeSlots = 16, kProbeItems = 12, kProbeStart = 13, kProbeEnd = 14;
+constexpr uint32_t kProbeWaves = 8192;  // waves recorded
 __device__ unsigned long long g_probe[kProbeWaves * kProbeSlots];
-#define QPP_PROBE_AT(i)                                                                      \
-    do {                                                                                     \
-        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                      \
-        const uint32_t w_ = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);             \
-        if (w_ < kProbeWaves && __lane_id() == __ffsll((long long)__ballot(1)) - 1)          \
-            g_probe[w_ * kProbeSlots + (i)] = t_;                                            \
+__device__ __forceinline__ unsigned long long *probe_marks()
+{
+    __shared__ unsigned long long m[16];
+    return m;
+}
+__device__ __forceinline__ void probe_mark(int i)
+{
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    const uint32_t wl = threadIdx.x >> 6, w = blockIdx.x * (blockDim.x / 64) + wl;
+    if (w < kProbeWaves && __lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+        unsigned long long *m = probe_marks();
+        unsigned long long *g = g_probe + (size_t)w * kProbeSlots;
+        if (i == kProbeStart) g[kProbeStart] = t;
+        else atomicAdd(&g[i], t - m[wl]);
+        g[kProbeEnd] = t;
+        m[wl] = t;
+    }
+}
+#define QPP_PROBE_AT(i) probe_mark(i)
+#define QPP_PROBE_COUNT()                                                                     \
+    do {                                                                                      \
+        const uint32_t w_ = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);              \
+        if (w_ < kProbeWaves && __lane_id() == __ffsll((long long)__ballot(1)) - 1)           \
+            atomicAdd(&g_probe[(size_t)w_ * kProbeSlots + kProbeItems], 1ull);                \
     } while (0)
 #else
+#define QPP_PROBE_COUNT() ((void)0)
 #define QPP_PROBE_AT(i) ((void)0)
 #endif
 
@@ -440,21 +461,29 @@ __device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, ui
 // staging slot, packet scratch) is recomputed from lane_fresh(): 128 VGPRs
 // leave no room to keep them live.  scr_wave = the wave's 16 packet
 // scratches, stage = the wave's 2 staging buffers, te = the AES image.
-// GHASH tables of the packet's key slot in LDS: four 8 KiB buffers at LDS
-// offset 0 (ghash_mul_lds selects one in its v_perm).  The wave's table word
-// (in LDS, re-read where needed rather than kept in SGPRs) says which buffer
-// holds H^1 (bits 0-3) and H^4 (bits 4-7); bit 8: all four powers are
-// resident (buffer p = H^(p+1)), so the last step can multiply every lane by
-// its own H^(4-j).
+// GHASH tables of the packet's key slot.  The step loop multiplies by H^4
+// from one of the workgroup's LDS table entries (8 KiB each at LDS offset 0;
+// ghash_mul_lds selects the entry in its v_perm).  The few multiplies outside
+// the loop (associated data beyond 16 bytes by H^1, each lane's closing
+// H^(4-j)) read the slot's tables in global memory, so that LDS holds H^4
+// alone and four connections' tables fit beside the AES image.  The wave's
+// slot and entry live in LDS, re-read where needed rather than kept in SGPRs.
 struct GhashTabs {
-    const uint8_t *base;
-    const uint32_t *wtab;
-    __device__ __forceinline__ uint32_t word() const
+    const uint8_t *lds;     // LDS table entries
+    const uint8_t *gtab;    // every slot's tables, global memory
+    const uint32_t *wslot;  // LDS: the wave's key slot
+    const uint32_t *went;   // LDS: the wave's table entry
+    __device__ __forceinline__ uint32_t t4() const
     {
-        return __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)wtab);
+        return __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)went) * (uint32_t)kGhashPowBytes;
+    }
+    // the slot's table of H^(pw + 1) in global memory
+    __device__ __forceinline__ const uint8_t *global(uint32_t pw) const
+    {
+        const uint32_t s = __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)wslot);
+        return gtab + (size_t)s * kGhashTabBytes + pw * (uint32_t)kGhashPowBytes;
     }
 };
-constexpr uint32_t kTabAll = 0x100u;
 
 template <int NR, bool ENC>
 __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int clen,
@@ -470,9 +499,9 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     const int n_g = za + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
     const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
     const bool tiny = rlen < 16;
-    // the H^4 buffer, read once: an LDS read inside the step loop would make
+    // the H^4 entry, read once: an LDS read inside the step loop would make
     // every step wait for all of its outstanding table lookups
-    const uint32_t t4 = ((G.word() >> 4) & 15u) * (uint32_t)kGhashPowBytes;
+    const uint32_t t4 = G.t4();
 
     if (tiny) *(u32x4 *)(scr + kScrTail) = ld_part(src, rlen);
 
@@ -493,7 +522,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         a = keep_bytes(a, min(16, hlen - 16 * g));
         if (!ENC && (hbits >> 28))
             a ^= hp_pattern(16 * g, hmask, hbits & 0xff, (hbits >> 8) & 0xffff, (hbits >> 24) & 0xf);
-        if (g > 0) z = ghash_mul_lds_narrow(z, G.base, (G.word() & 15u) * (uint32_t)kGhashPowBytes);  // H^1
+        if (g > 0) z = ghash_mul_global(z, G.global(0));  // H^1
         z ^= a;
     }
     u32x4 acc = (za && sub == pad) ? z : u32x4{0, 0, 0, 0};
@@ -533,7 +562,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         __builtin_amdgcn_sched_barrier(0);
         // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
         // is applied after the loop
-        if (!last) acc = ghash_mul_lds(acc, G.base, t4);
+        if (!last) acc = ghash_mul_lds(acc, G.lds, t4);
     };
     // buffer offset of CT block i's input (or out of range)
     auto ct_load = [&](int i) -> uint32_t {
@@ -544,7 +573,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     got_tag = u32x4{0, 0, 0, 0};
     if (tiny) {
         // < 16 input bytes: one step (n_a, n_c <= 1), input from LDS
-        QPP_PROBE_AT(3);
+        QPP_PROBE_AT(4);
         // the staged bytes as an end-aligned load would see them
         const u32x4 st = *(const u32x4 *)(scr + kScrTail);
         step(sub - q, true, true, shl_bytes(st, 16 - rlen));
@@ -557,7 +586,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         };
         int i = sub - q, b = 0;
         dma(ct_load(i), 0);
-        QPP_PROBE_AT(3);
+        QPP_PROBE_AT(4);
         const uint32_t waves = blockDim.x >> 6;
         uint32_t it = 0;
         for (int k = S; k > 0; --k, i += 4, b ^= 1) {
@@ -592,35 +621,16 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
     }
+    QPP_PROBE_AT(5);
     // lane-derived values recomputed after the loop rather than kept (spilled)
     const uint32_t lf = lane_fresh();
-    const uint32_t tw = G.word();
-    if (tw & kTabAll) {
-        // every power resident: lane j multiplies by H^(4-j) (buffer 3 - j)
-        acc = ghash_mul_lds_narrow(acc, G.base, (uint32_t)(3 - (lf & 3)) * (uint32_t)kGhashPowBytes);
-        // the lengths block is the last of the sequence: lane 3, last step
-        __builtin_amdgcn_wave_barrier();
-        if ((lf & 3) == 3) acc ^= *(const u32x4 *)(scr_wave + (lf >> 2) * kScratch + kScrEj0);
-        return quad_xor_all(acc);
-    }
-    // H^1 and H^4 only: sum_j acc_j H^(4-j) = (((acc_0 H + acc_1) H + acc_2) H + acc_3) H,
-    // one step per lane of the quad, lane 3 ending with the sum
-    const uint32_t t1 = (tw & 15u) * (uint32_t)kGhashPowBytes;
-    u32x4 t = zero4();
-#pragma unroll 1
-    for (int j = 0; j < 4; ++j) {
-        u32x4 prev;  // lane i <- lane i-1's t, lane 0 <- 0
-        prev.x = quad_perm<0x90>(t.x);
-        prev.y = quad_perm<0x90>(t.y);
-        prev.z = quad_perm<0x90>(t.z);
-        prev.w = quad_perm<0x90>(t.w);
-        if ((lane_fresh() & 3) == 0) prev = zero4();
-        t = ghash_mul_lds_narrow(prev ^ acc, G.base, t1);
-    }
+    // lane j closes its Horner chain with H^(4-j) (the slot's global table
+    // of power 3 - j): sum_j acc_j H^(4-j) after the quad's xor
+    acc = ghash_mul_global(acc, G.global(3u - (lf & 3)));
+    // the lengths block is the last of the sequence: lane 3, last step
     __builtin_amdgcn_wave_barrier();
-    const uint32_t l2 = lane_fresh();
-    if ((l2 & 3) == 3) t ^= *(const u32x4 *)(scr_wave + (l2 >> 2) * kScratch + kScrEj0);
-    return u32x4{quad_perm<0xFF>(t.x), quad_perm<0xFF>(t.y), quad_perm<0xFF>(t.z), quad_perm<0xFF>(t.w)};
+    if ((lf & 3) == 3) acc ^= *(const u32x4 *)(scr_wave + (lf >> 2) * kScratch + kScrEj0);
+    return quad_xor_all(acc);
 }
 
 // Output side of a GCM packet after the step loop: partial tail block, tag,
@@ -841,53 +851,298 @@ __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int su
 // [irange[2 SUITE], irange[2 SUITE + 1]) (wave_span), and a packet's result
 // goes to res[desc.rsv] (its index in the caller's order).
 
-// GCM: the workgroup's 32 KiB of GHASH table buffers hold either all four
-// powers of its one key slot, or H^1 and H^4 of each of its two lowest slots,
-// so the waves of a workgroup whose 256 packets span two connections (a
-// bucketed server batch: ~2 slots per workgroup at 4096 keys per Mi packets)
-// each run their own slot without waiting for the others.  Further slots
-// (rare once bucketed) run one after the other through buffers 0 and 1.
-constexpr int kResident = 2;
+// GCM: a persistent kernel, one 1024-thread workgroup per CU (its LDS use
+// allows no second one).  The workgroup fills the AES image once and then
+// works through a contiguous share of the launch's wave items: each wave
+// takes the next item of the share (an LDS counter) as soon as it finishes
+// the last, so no wave waits for the others and no CU idles between
+// workgroups.  An item is <= 16 packets (one per quad): planned, one key
+// slot's run (qpp_plan.hip); unplanned, 16 consecutive positions.
+//
+// GHASH tables: kTabEntries LDS entries, each the H^4 table of one key slot,
+// shared by the waves running that slot (a reference count per entry).  A
+// wave that needs a slot no entry holds loads it into the least recently
+// used free entry (LDS-DMA, 8 KiB); with every entry in use by other slots
+// it waits for one to come free.  A share of a bucketed batch walks its
+// slots in order, so the 16 waves hold one or two slots at a time.
+constexpr int kTabEntries = 4;
 
 template <int WG>
 struct __attribute__((aligned(16))) GcmSmem {
-    // GHASH table buffers first (LDS offset 0: ghash_mul_lds adds b * 8 KiB in
+    // GHASH table entries first (LDS offset 0: ghash_mul_lds adds e * 8 KiB in
     // its v_perm), then the AES image at 32 KiB; both within the 16-bit
     // ds_read immediate range
-    uint8_t h4[4][kGhashPowBytes];           // 32 KiB
-    uint8_t te[kTeBytes];                    // Te0|Te1 x 32 bank copies   64 KiB
+    uint8_t h4[kTabEntries][kGhashPowBytes];  // 32 KiB
+    uint8_t te[kTeBytes];                     // Te0|Te1 x 32 bank copies   64 KiB
     uint8_t scratch[WG / 4][kScratch];
-    uint8_t stage[WG / 64][2][kStageBytes];  // per-wave LDS-DMA input staging
-    uint32_t resident[kResident];            // slots of the resident tables (kNoSlot: none)
-    uint32_t wslot[WG / 64];                 // per wave: the slot it is running
-    uint32_t wtab[WG / 64];                  // per wave: its GhashTabs word
-    uint32_t wlast[WG / 64];                 // per wave: the last slot it ran
-    uint32_t more;                           // lowest slot beyond the resident ones (fallback)
-    uint32_t cur[2];                         // fallback: the slot being run / the next one
-    uint32_t progress;                       // steps done by the workgroup's waves (wave balancing)
+    uint8_t stage[WG / 64][2][kStageBytes];   // per-wave LDS-DMA input staging
+    uint32_t eslot[kTabEntries];              // slot held by entry e (kNoSlot: none)
+    uint32_t eref[kTabEntries];               // waves running entry e's slot
+    uint32_t eready[kTabEntries];             // entry e's table has landed
+    uint32_t eused[kTabEntries];              // last acquisition (LRU tick)
+    uint32_t lock, tick, next;                // entry lock; LRU clock; next item of the share
+    uint32_t wslot[WG / 64];                  // per wave: the slot it is running
+    uint32_t went[WG / 64];                   // per wave: that slot's table entry
 };
 
-// LDS-DMA of slot s's table of H^(p+1) (8 KiB) into table buffer r: 1 KiB
-// pieces spread over the workgroup's waves.  Retired by the caller
-// (vmcnt(0) + barrier) before use.
+// Entry of slot `cur` for the calling wave (wave-uniform control flow):
+// found, or loaded into a free entry.  Lane 0 does the bookkeeping under the
+// workgroup's LDS lock.  Returns once the entry's table is in LDS.
 template <int WG>
-__device__ __forceinline__ void stage_pow(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t s, int p, int r,
-                                          int w0)
+__device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t cur)
 {
     typedef const __attribute__((address_space(1))) void *gptr_t;
     typedef __attribute__((address_space(3))) void *lptr_t;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = (int)lane_fresh();
-    const uint8_t *src = gtab + (size_t)s * kGhashTabBytes + p * kGhashPowBytes;
-    for (int c = (w + w0) % (WG / 64); c < kGhashPowBytes / 1024; c += WG / 64)
-        __builtin_amdgcn_global_load_lds((gptr_t)(src + c * 1024 + l * 16), (lptr_t)(sm.h4[r] + c * 1024),
-                                         16, 0, 0);
+    uint32_t e = kNoSlot, load = 0;
+    // bounded: every entry in use means other waves are running their slots,
+    // and each of them releases its entry when done (watchdog, not a limit
+    // that a correct run reaches: ~1 s of sleeps)
+#pragma unroll 1
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+        uint32_t got = kNoSlot, ld = 0;
+        if (lane_fresh() == 0) {
+            while (atomicCAS(&sm.lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
+            int hit = -1, vic = -1;
+            uint32_t best = 0xffffffffu;
+#pragma unroll
+            for (int i = 0; i < kTabEntries; ++i) {
+                const uint32_t s = ((volatile uint32_t *)sm.eslot)[i];
+                const uint32_t r = ((volatile uint32_t *)sm.eref)[i];
+                const uint32_t u = ((volatile uint32_t *)sm.eused)[i];
+                if (s == cur) hit = i;
+                else if (r == 0u && u < best) {
+                    best = u;
+                    vic = i;
+                }
+            }
+            if (hit < 0 && vic >= 0) {
+                hit = vic;
+                ld = 1;
+                ((volatile uint32_t *)sm.eslot)[vic] = cur;
+                ((volatile uint32_t *)sm.eready)[vic] = 0u;
+            }
+            if (hit >= 0) {
+                got = (uint32_t)hit;
+                atomicAdd(&sm.eref[hit], 1u);  // atomic: releases decrement without the lock
+                const uint32_t t = ((volatile uint32_t *)&sm.tick)[0] + 1u;
+                ((volatile uint32_t *)&sm.tick)[0] = t;
+                ((volatile uint32_t *)sm.eused)[hit] = t;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // bookkeeping before the unlock
+            atomicExch(&sm.lock, 0u);
+        }
+        got = __builtin_amdgcn_readfirstlane(got);
+        if (got != kNoSlot) {
+            e = got;
+            load = __builtin_amdgcn_readfirstlane(ld);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if (e == kNoSlot) return e;  // watchdog: no entry came free (the slot's packets are skipped)
+    if (load) {
+        // H^4 (power 3) of the slot: 8 pieces of 1 KiB
+        const uint8_t *src = gtab + (size_t)cur * kGhashTabBytes + 3 * kGhashPowBytes;
+        const uint32_t l = lane_fresh();
+#pragma unroll
+        for (int c = 0; c < kGhashPowBytes / 1024; ++c)
+            __builtin_amdgcn_global_load_lds((gptr_t)(src + c * 1024 + l * 16), (lptr_t)(sm.h4[e] + c * 1024),
+                                             16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane_fresh() == 0) ((volatile uint32_t *)sm.eready)[e] = 1u;
+    } else {
+#pragma unroll 1
+        for (int spin = 0; spin < (1 << 22); ++spin) {
+            if (__builtin_amdgcn_readfirstlane(((volatile uint32_t *)sm.eready)[e])) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    return e;
+}
+
+template <int WG>
+__device__ __forceinline__ void tab_release(GcmSmem<WG> &sm, uint32_t e)
+{
+    if (lane_fresh() == 0) atomicSub(&sm.eref[e], 1u);
+}
+
+template <int SUITE, bool ENC, int WG>
+__global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots,
+                                              const uint8_t *__restrict__ gtab, uint32_t cap,
+                                              const qpp_desc *__restrict__ desc, uint32_t n,
+                                              const uint8_t *gin, uint8_t *gout,
+                                              qpp_result *__restrict__ res,
+                                              const uint32_t *__restrict__ items,
+                                              const uint32_t *__restrict__ irange)
+{
+    constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    QPP_PROBE_AT(kProbeStart);
+    const bool planned = irange != nullptr;
+    // this workgroup's share [sb, se) of the launch's items
+    uint32_t ib = 0, ie = (n + 15u) / 16u;
+    if (planned) {
+        ib = irange[2 * SUITE];
+        ie = irange[2 * SUITE + 1];
+    }
+    const uint32_t total = ie > ib ? ie - ib : 0u;
+    const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
+    const uint32_t sb = ib + min(total, per * blockIdx.x), se = ib + min(total, per * (blockIdx.x + 1));
+    if (sb >= se) return;  // uniform over the workgroup
+    __shared__ GcmSmem<WG> sm;
+    // Thread-derived values are recomputed where they are used, from the
+    // wave index (an SGPR) and a fresh lane id, instead of being kept live
+    // across the packet loops: at 128 VGPRs anything live across the GCM step
+    // loop is spilled to scratch (HBM traffic and latency).
+    auto tid_now = [&]() -> uint32_t { return (wv << 6) | lane_fresh(); };
+    load_te<WG>(sm.te);
+    if (threadIdx.x < kTabEntries) {
+        sm.eslot[threadIdx.x] = kNoSlot;
+        sm.eref[threadIdx.x] = 0u;
+        sm.eready[threadIdx.x] = 0u;
+        sm.eused[threadIdx.x] = 0u;
+    }
+    if (threadIdx.x == 0) {
+        sm.lock = 0u;
+        sm.tick = 0u;
+        sm.next = sb;
+    }
+    __syncthreads();
+    QPP_PROBE_AT(0);  // prologue
+
+#pragma unroll 1
+    for (;;) {
+        uint32_t j = 0;
+        if (lane_fresh() == 0) j = atomicAdd(&sm.next, 1u);
+        j = __builtin_amdgcn_readfirstlane(j);
+        if (j >= se) break;
+        QPP_PROBE_AT(1);  // the previous item's tail, the grab
+        QPP_PROBE_COUNT();
+        // the item's positions [wb, we) of desc
+        uint32_t wb, we;
+        if (planned) {
+            wb = __builtin_amdgcn_readfirstlane(items[j]);
+            we = __builtin_amdgcn_readfirstlane(items[j + 1]);
+        } else {
+            wb = 16u * j;
+            we = min(n, wb + 16u);
+        }
+        auto pkt_of = [&](uint32_t t) -> uint32_t { return wb + ((t & 63) >> 2); };
+        // a lane's key slot, or kNoSlot (no packet, or a slot beyond the table)
+        auto slot_of = [&](const qpp_desc &d, uint32_t p) -> uint32_t {
+            return (p < we && d.slot < cap) ? d.slot : kNoSlot;
+        };
+        // 32-bit buffer views based at the item's lowest input / output
+        // offsets (an item's packets must lie within 4 GiB of each other);
+        // slots beyond the table: KeyUnavailableError
+        uint64_t bi, bo;
+        {
+            const uint32_t t = tid_now(), p = pkt_of(t);
+            uint64_t in0 = ~0ull, out0 = ~0ull;
+            if (p < we) {
+                const qpp_desc d = desc[p];
+                in0 = d.in_off;
+                out0 = d.out_off;
+                if (d.slot >= cap && (t & 3) == 0) res[planned ? d.rsv : p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+            }
+            bi = wave_min_u64(in0);
+            bo = wave_min_u64(out0);
+        }
+
+        // The packets of one key slot `cur` among the item's
+        auto run_slot = [&](uint32_t cur) {
+            const KeySlot *ks = slots + cur;
+            const uint32_t t1 = tid_now(), p1 = pkt_of(t1);
+            const qpp_desc d = p1 < we ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
+            if (slot_of(d, p1) != cur) return;  // the lambda's only early exit, at its top
+            const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
+            const LdsTe T{sm.te, (t1 & 31) * 4};
+            Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
+            if (P.status == QPP_S_OK) {
+                // plain keys for rounds 0-2 (counter cache) and NR, rotated between
+                uint32_t rk[4 * (kNR + 1)];
+#pragma unroll
+                for (int i = 0; i < 4 * (kNR + 1); ++i)
+                    rk[i] = __builtin_amdgcn_readfirstlane((i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
+                const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
+                const uint64_t rlen = (uint64_t)(P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN));
+                const uint64_t wlen = (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN);
+                if (ioff + rlen <= kBufBytes && ooff + wlen <= kBufBytes) {
+                    const Bufs B{
+                        __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
+                        __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
+                    uint8_t *scr = sm.scratch[t1 >> 2];
+                    const int hlen = P.hlen, clen = P.clen;
+                    const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 |
+                                           (uint32_t)P.hp << 28;
+                    park(P, scr);
+                    *(u32x4 *)(scr + kScrHdr) = pre.h0;
+                    QPP_PROBE_AT(3);
+                    const GhashTabs G{&sm.h4[0][0], gtab, &sm.wslot[wv], &sm.went[wv]};
+                    u32x4 got_tag;
+                    const u32x4 tag = gcm_packet<kNR, ENC>(
+                        P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
+                        (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0], nullptr,
+                        got_tag);
+                    QPP_PROBE_AT(6);
+                    // everything below is re-derived after the step loop
+                    const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
+                    const qpp_desc d2 = desc[p2];
+                    uint8_t *scr2 = sm.scratch[t2 >> 2];
+                    P = unpark(scr2, gin + d2.in_off, gout + d2.out_off);
+                    const LdsTe T2{sm.te, (t2 & 31) * 4};
+                    const KeySlot *ks2 =
+                        slots + __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
+                    gcm_finish<ENC, SUITE>(P, ks2, t2 & 3, scr2, T2, tag, got_tag);
+                } else {
+                    P.status = QPP_S_LENGTH;  // the item spans more than 4 GiB
+                }
+            }
+            const uint32_t t3 = tid_now(), p3 = pkt_of(t3);
+            write_result<ENC>(res, planned ? desc[p3].rsv : p3, t3 & 3, P);
+            QPP_PROBE_AT(7);
+        };
+
+        // slot by slot among the item's packets, lowest first (planned: one);
+        // bounded: an item holds at most 16 distinct slots (watchdog against
+        // a logic error turning into a hung GPU)
+        uint32_t last = kNoSlot;
+#pragma unroll 1
+        for (int guard = 0; guard < 17; ++guard) {
+            const uint32_t t = tid_now(), p = pkt_of(t);
+            const uint32_t s = p < we ? slot_of(desc[p], p) : kNoSlot;
+            const uint32_t cur = wave_min_u32((last == kNoSlot || s > last) ? s : kNoSlot);
+            if (cur == kNoSlot) break;
+            last = cur;
+            const uint32_t suite = __builtin_amdgcn_readfirstlane(slots[cur].suite);
+            if (suite > QPP_CHACHA20_POLY1305) {
+                // an empty slot: KeyUnavailableError (every suite's launch writes the same)
+                if (s == cur && (t & 3) == 0) {
+                    const qpp_desc d = desc[p];
+                    res[planned ? d.rsv : p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+                }
+                continue;
+            }
+            if (suite != SUITE) continue;  // another suite's launch
+            QPP_PROBE_AT(1);
+            const uint32_t e = tab_acquire<WG>(sm, gtab, cur);
+            QPP_PROBE_AT(2);  // table entry
+            if (e == kNoSlot) continue;
+            if (lane_fresh() == 0) {
+                sm.wslot[wv] = cur;
+                sm.went[wv] = e;
+            }
+            run_slot(cur);
+            tab_release<WG>(sm, e);
+            QPP_PROBE_AT(8);
+        }
+    }
+    QPP_PROBE_AT(9);
 }
 
 // The packets of one wave: positions [b, e) of desc.  Unplanned: 16
 // consecutive positions per wave.  Planned: the wave's item of the plan (<= 16
-// positions on one key slot, qpp_plan.hip), so that no wave straddles two
-// slots -- a straddling wave runs its packets in two passes and holds its
-// workgroup (one per CU) for twice as long.  empty_wg: the whole workgroup is
+// positions on one key slot, qpp_plan.hip).  empty_wg: the whole workgroup is
 // past the batch / the suite's items (uniform, so it may return before any
 // barrier).
 struct WaveSpan {
@@ -916,213 +1171,6 @@ __device__ __forceinline__ WaveSpan wave_span(uint32_t n, const uint32_t *items,
         w.e = w.b < n ? min(n, w.b + 16u) : w.b;
     }
     return w;
-}
-
-template <int SUITE, bool ENC, int WG>
-__global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots,
-                                              const uint8_t *__restrict__ gtab, uint32_t cap,
-                                              const qpp_desc *__restrict__ desc, uint32_t n,
-                                              const uint8_t *gin, uint8_t *gout,
-                                              qpp_result *__restrict__ res,
-                                              const uint32_t *__restrict__ items,
-                                              const uint32_t *__restrict__ irange)
-{
-    constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, wv);
-    if (W.empty_wg) return;  // past this suite's bucket
-    const uint32_t wb = W.b, we = W.e, planned = irange != nullptr;
-    __shared__ GcmSmem<WG> sm;
-    // Thread-derived values are recomputed where they are used, from the
-    // wave index (an SGPR) and a fresh lane id, instead of being kept live
-    // across the packet loops: at 128 VGPRs anything live across the GCM step
-    // loop is spilled to scratch (HBM traffic and latency).
-    auto tid_now = [&]() -> uint32_t { return (wv << 6) | lane_fresh(); };
-    auto pkt_of = [&](uint32_t t) -> uint32_t { return wb + ((t & 63) >> 2); };
-    // a lane's key slot, or kNoSlot (no packet, or a slot beyond the table)
-    auto slot_of = [&](const qpp_desc &d, uint32_t p) -> uint32_t {
-        return (p < we && d.slot < cap) ? d.slot : kNoSlot;
-    };
-    QPP_PROBE_AT(0);
-
-    // Prologue: descriptor, the workgroup's resident slots (its lowest
-    // distinct slots, one min-reduction each), their H^4 tables and the AES
-    // image into LDS.
-    uint64_t in0 = ~0ull, out0 = ~0ull;
-    uint32_t my_slot = kNoSlot;
-    {
-        const uint32_t p = pkt_of(threadIdx.x);
-        qpp_desc d = {};
-        if (p < we) d = desc[p];
-        my_slot = slot_of(d, p);
-        if (p < we) {
-            in0 = d.in_off;
-            out0 = d.out_off;
-        }
-        if (threadIdx.x < kResident) sm.resident[threadIdx.x] = kNoSlot;
-        if (threadIdx.x == 0) {
-            sm.more = kNoSlot;
-            sm.progress = 0;
-        }
-    }
-    load_te<WG>(sm.te);
-    __syncthreads();
-    uint32_t lo = 0;
-    int nres = 0;
-    for (int r = 0; r <= kResident; ++r) {
-        const uint32_t m = wave_min_u32(my_slot >= lo ? my_slot : kNoSlot);
-        uint32_t *dst = r < kResident ? &sm.resident[r] : &sm.more;
-        if (__lane_id() == 0 && m != kNoSlot) atomicMin(dst, m);
-        __syncthreads();
-        const uint32_t got = __builtin_amdgcn_readfirstlane(*dst);
-        if (got == kNoSlot) break;
-        if (r < kResident) ++nres;
-        lo = got + 1;
-    }
-    // one slot: its four powers in buffers 0..3; two: H^1, H^4 of slot r in 2r, 2r + 1
-    for (int r = 0; r < nres; ++r) {
-        const uint32_t sl = __builtin_amdgcn_readfirstlane(sm.resident[r]);
-        if (slots[sl].suite != SUITE) continue;
-        if (nres == 1) {
-            for (int pw = 0; pw < 4; ++pw) stage_pow<WG>(sm, gtab, sl, pw, pw, 4 * pw);
-        } else {
-            stage_pow<WG>(sm, gtab, sl, 0, 2 * r, 8 * r);
-            stage_pow<WG>(sm, gtab, sl, 3, 2 * r + 1, 8 * r + 4);
-        }
-    }
-    // 32-bit buffer views based at this wave's lowest input / output offsets
-    // (a wave's 16 packets must lie within 4 GiB of each other); wave-uniform
-    const uint64_t bi = wave_min_u64(in0);
-    const uint64_t bo = wave_min_u64(out0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident tables (LDS-DMA)
-    __syncthreads();
-    QPP_PROBE_AT(7);
-
-    // The packets of one key slot `cur` among this wave's 16 (table buffer tb)
-    auto run_slot = [&](uint32_t cur, uint32_t tab_word) {
-        if (lane_fresh() == 0) {
-            sm.wslot[wv] = cur;
-            sm.wtab[wv] = tab_word;
-        }
-        const KeySlot *ks = slots + cur;
-        const uint32_t suite = ks->suite;
-        const uint32_t t1 = tid_now(), p1 = pkt_of(t1);
-        const qpp_desc d = p1 < we ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
-        const bool mine = slot_of(d, p1) == cur;
-        // an empty slot: KeyUnavailableError (every suite's launch writes the same)
-        if (mine && suite > QPP_CHACHA20_POLY1305 && (t1 & 3) == 0)
-            res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
-        if (!mine || suite != SUITE) return;  // the lambda's only early exit, at its top
-        const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
-        const LdsTe T{sm.te, (t1 & 31) * 4};
-        Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
-        if (P.status == QPP_S_OK) {
-            // plain keys for rounds 0-2 (counter cache) and NR, rotated between
-            uint32_t rk[4 * (kNR + 1)];
-#pragma unroll
-            for (int i = 0; i < 4 * (kNR + 1); ++i)
-                rk[i] = __builtin_amdgcn_readfirstlane((i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
-            const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
-            const uint64_t rlen = (uint64_t)(P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN));
-            const uint64_t wlen = (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN);
-            if (ioff + rlen <= kBufBytes && ooff + wlen <= kBufBytes) {
-                const Bufs B{
-                    __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
-                    __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
-                uint8_t *scr = sm.scratch[t1 >> 2];
-                const int hlen = P.hlen, clen = P.clen;
-                const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 |
-                                       (uint32_t)P.hp << 28;
-                park(P, scr);
-                *(u32x4 *)(scr + kScrHdr) = pre.h0;
-                QPP_PROBE_AT(2);
-                const GhashTabs G{&sm.h4[0][0], &sm.wtab[wv]};
-                u32x4 got_tag;
-                const u32x4 tag = gcm_packet<kNR, ENC>(
-                    P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
-                    (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0],
-                    (kBalance && (!ENC || kBalanceEnc)) ? &sm.progress : nullptr, got_tag);
-                QPP_PROBE_AT(4);
-                // everything below is re-derived after the step loop
-                const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
-                const qpp_desc d2 = desc[p2];
-                uint8_t *scr2 = sm.scratch[t2 >> 2];
-                P = unpark(scr2, gin + d2.in_off, gout + d2.out_off);
-                const LdsTe T2{sm.te, (t2 & 31) * 4};
-                const KeySlot *ks2 = slots + __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
-                gcm_finish<ENC, SUITE>(P, ks2, t2 & 3, scr2, T2, tag, got_tag);
-            } else {
-                P.status = QPP_S_LENGTH;  // the wave spans more than 4 GiB
-            }
-        }
-        const uint32_t t3 = tid_now(), p3 = pkt_of(t3);
-        write_result<ENC>(res, planned ? desc[p3].rsv : p3, t3 & 3, P);
-        QPP_PROBE_AT(5);
-    };
-
-    // Main phase: each wave on its own, slot by slot among its packets
-    // (lowest first; usually one), for the resident slots (those <= the last
-    // resident one).  A packet is done once its slot is <= the last run.
-    // (loop state lives in LDS: SGPRs are scarce across the step loop)
-    if (lane_fresh() == 0) sm.wlast[wv] = kNoSlot;
-    // bounded: a wave holds at most 16 distinct slots (watchdog against a
-    // logic error turning into a hung GPU)
-    #pragma unroll 1
-    for (int guard = 0; guard < 17; ++guard) {
-        const uint32_t more = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.more);
-        const uint32_t res_hi = more == kNoSlot ? 0xfffffffeu
-                                                : __builtin_amdgcn_readfirstlane(sm.resident[kResident - 1]);
-        const uint32_t last = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wlast[wv]);
-        const uint32_t t = tid_now(), p = pkt_of(t);
-        const qpp_desc d = p < we ? desc[p] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
-        const uint32_t s = slot_of(d, p);
-        const uint32_t cur = wave_min_u32((s <= res_hi && (last == kNoSlot || s > last)) ? s : kNoSlot);
-        if (cur == kNoSlot) break;
-        // table word: one resident slot -> all powers; else H^1 / H^4 of its pair
-        const bool single = __builtin_amdgcn_readfirstlane(sm.resident[1]) == kNoSlot;
-        const uint32_t tw = single ? (0u | 3u << 4 | kTabAll)
-                                   : (__builtin_amdgcn_readfirstlane(sm.resident[0]) == cur ? (0u | 1u << 4)
-                                                                                           : (2u | 3u << 4));
-        if (lane_fresh() == 0) sm.wlast[wv] = cur;
-        run_slot(cur, tw);
-    }
-    // packets whose slot lies beyond the table: KeyUnavailableError
-    {
-        const uint32_t t = tid_now(), p = pkt_of(t);
-        if (p < we && (t & 3) == 0) {
-            const qpp_desc d = desc[p];
-            if (d.slot >= cap) res[planned ? d.rsv : p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
-        }
-    }
-    // Fallback phase, only when the workgroup holds more than kResident
-    // slots: the remaining ones one after the other through table buffer 0,
-    // the whole workgroup together.
-    if (__builtin_amdgcn_readfirstlane(sm.more) != kNoSlot) {
-        __syncthreads();
-        if (threadIdx.x == 0) sm.cur[0] = __builtin_amdgcn_readfirstlane(sm.more);
-        __syncthreads();
-        for (int it = 0; it < WG / 4; ++it) {  // at most one per packet
-            const uint32_t cur = __builtin_amdgcn_readfirstlane(sm.cur[it & 1]);
-            if (cur == kNoSlot) break;
-            if (slots[cur].suite == SUITE) {
-                stage_pow<WG>(sm, gtab, cur, 0, 0, 0);
-                stage_pow<WG>(sm, gtab, cur, 3, 1, 8);
-            }
-            if (wv == 0 && lane_fresh() == 0) sm.cur[(it + 1) & 1] = kNoSlot;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            {
-                const uint32_t t = tid_now(), p = pkt_of(t);
-                const qpp_desc d = p < we ? desc[p] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
-                const uint32_t s = slot_of(d, p);
-                const uint32_t m = wave_min_u32(s > cur ? s : kNoSlot);
-                if (__lane_id() == 0 && m != kNoSlot) atomicMin(&sm.cur[(it + 1) & 1], m);
-            }
-            run_slot(cur, 0u | 1u << 4);
-            __syncthreads();
-        }
-    }
-    QPP_PROBE_AT(6);
 }
 
 // ChaCha20-Poly1305: no tables, so every wave runs its packets slot by slot
@@ -1576,6 +1624,27 @@ static int wg_choice(const char *env, int dflt, bool chacha)
     return (w == 512 || w == 768 || w == 1024) ? w : dflt;
 }
 
+// Persistent GCM grid: one workgroup per CU (the kernel's LDS admits no
+// second), fewer when the batch has fewer than a workgroup's worth of items
+// per CU.
+static uint32_t gcm_grid(uint32_t items, uint32_t waves_per_wg)
+{
+    static int cus[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (!cus[dev]) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) {
+            (void)hipGetLastError();
+            c = 256;
+        }
+        cus[dev] = c;
+    }
+    const uint32_t need = (items + waves_per_wg - 1) / waves_per_wg;
+    return need < (uint32_t)cus[dev] ? (need ? need : 1u) : (uint32_t)cus[dev];
+}
+
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                           const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream,
                           const qpp_plan *plan = nullptr)
@@ -1596,7 +1665,7 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
                           : wg_choice("QPP_WG_CHACHA_DEC", kChachaWGDec, true);
 #define QPP_LAUNCH_GCM_WG(SUITE, WGV)                                                          \
     do {                                                                                       \
-        const dim3 grid((waves + WGV / 64 - 1) / (WGV / 64)), block(WGV);                      \
+        const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
         if (enc)                                                                               \
             hipLaunchKernelGGL((k_gcm<SUITE, true, WGV>), grid, block, 0, s, kt->d_slots,      \
                                kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_items,    \

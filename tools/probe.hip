@@ -1,7 +1,7 @@
 // Phase-timing probe of the packet kernels: the engine built with -DQPP_PROBE,
-// 64Ki x 1200 B AES-128-GCM (the bench workload), per-wave timestamps.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -DQPP_PROBE \
-//            -o tools/probe tools/probe.hip
+// n x 1200 B AES-128-GCM (default 1 Mi, the bench workload), per-wave phase sums.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -DQPP_PROBE -c -o /tmp/probe.o tools/probe.hip && \
+//        hipcc --offload-arch=gfx950 -o tools/probe /tmp/probe.o build/obj/qpp_plan.o
 // Run:   tools/probe [packets] [suite]
 #include <stdio.h>
 #include <stdlib.h>
@@ -19,48 +19,52 @@ static void fill(uint8_t *p, size_t n, uint32_t seed)
     }
 }
 
-static void report(const char *what, const std::vector<unsigned long long> &pr, int waves)
+static void report(const char *what, const std::vector<unsigned long long> &pr)
 {
-    const char *names[] = {"  desc load", "  load_te", "  hdr prefetch", "  sync 1", "  atomics + sync 2", "prologue (te, desc, hdr, 2 syncs)", "slot + GHASH table", "pkt_begin",
-                           "AAD fold + ctr cache", "step loop", "finish + result", "final sync"};
-    const int from[] = {0, 10, 11, 12, 13, 0, 7, 1, 2, 3, 4, 5}, to[] = {10, 11, 12, 13, 7, 7, 1, 2, 3, 4, 5, 6};
-    constexpr int NP = 12;
-    unsigned long long t0 = ~0ull, t1 = 0;
-    for (int w = 0; w < waves; ++w) {
-        t0 = std::min(t0, pr[w * 16 + 0]);
-        t1 = std::max(t1, pr[w * 16 + 6]);
-    }
-    printf("%s: waves %d, span %.2f us\n", what, waves, (t1 - t0) / 100.0);
-    for (int ph = 0; ph < NP; ++ph) {
-        double sum = 0, mx = 0;
-        for (int w = 0; w < waves; ++w) {
-            const double d = (double)(pr[w * 16 + to[ph]] - pr[w * 16 + from[ph]]) / 100.0;
-            sum += d;
-            mx = std::max(mx, d);
+    // phases of the persistent GCM kernel (qpp_engine.hip QPP_PROBE_AT marks)
+    const char *names[] = {"prologue (AES image, entry init, sync)", "item tail + grab", "table entry (acquire)",
+                           "descriptor, pkt_begin, park", "AAD fold + counter cache", "step loop",
+                           "closing GHASH multiply (global tables)", "finish: tail, tag, header, result",
+                           "release", "exit"};
+    constexpr int NP = 10;
+    int waves = 0;
+    unsigned long long t0 = ~0ull, t1 = 0, items = 0;
+    double sum[NP] = {}, mx[NP] = {};
+    for (int w = 0; w < kProbeWaves; ++w) {
+        const unsigned long long *g = &pr[(size_t)w * kProbeSlots];
+        if (!g[kProbeStart]) continue;
+        ++waves;
+        t0 = std::min(t0, g[kProbeStart]);
+        t1 = std::max(t1, g[kProbeEnd]);
+        items += g[kProbeItems];
+        for (int ph = 0; ph < NP; ++ph) {
+            sum[ph] += g[ph] / 100.0;
+            mx[ph] = std::max(mx[ph], g[ph] / 100.0);
         }
-        printf("  %-34s mean %8.2f us  max %8.2f us\n", names[ph], sum / waves, mx);
     }
-    // start / end spread
-    double s_max = 0, e_min = 1e30;
-    for (int w = 0; w < waves; ++w) {
-        s_max = std::max(s_max, (pr[w * 16 + 0] - t0) / 100.0);
-        e_min = std::min(e_min, (pr[w * 16 + 6] - t0) / 100.0);
+    if (!waves) { printf("%s: no probe data\n", what); return; }
+    printf("%s: waves %d, items %llu (%.1f per wave), span %.2f us\n", what, waves, items,
+           (double)items / waves, (t1 - t0) / 100.0);
+    double tot = 0;
+    for (int ph = 0; ph < NP; ++ph) tot += sum[ph];
+    for (int ph = 0; ph < NP; ++ph)
+        printf("  %-40s per wave mean %9.2f us (%5.1f %%)  max %9.2f us  per item %7.3f us\n", names[ph],
+               sum[ph] / waves, 100.0 * sum[ph] / tot, mx[ph], sum[ph] / (double)items);
+    double e_min = 1e30, e_max = 0;
+    for (int w = 0; w < kProbeWaves; ++w) {
+        const unsigned long long *g = &pr[(size_t)w * kProbeSlots];
+        if (!g[kProbeStart]) continue;
+        e_min = std::min(e_min, (g[kProbeEnd] - t0) / 100.0);
+        e_max = std::max(e_max, (g[kProbeEnd] - t0) / 100.0);
     }
-    printf("  last wave start %.2f us, first wave end %.2f us\n", s_max, e_min);
+    printf("  wave ends: first %.2f us, last %.2f us\n", e_min, e_max);
 }
 
 int main(int argc, char **argv)
 {
-    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 65536;
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 20);
     const int suite = argc > 2 ? atoi(argv[2]) : 0;
-#ifdef QPP_PROBE
-    if (n == 0 || n > kProbeWaves * 16) {  // 16 packets per wave are recorded
-        printf("probe: n must be 1..%u\n", kProbeWaves * 16);
-        return 2;
-    }
-#else
     if (n == 0) return 2;
-#endif
     // header length (argv[4], default 11): 16 puts every ciphertext block on a 16-byte boundary
     const int hdr = argc > 4 ? atoi(argv[4]) : 11, slot = 1200, payload = slot - 16 - hdr;
     qpp_keytab *kt = nullptr;
@@ -124,8 +128,9 @@ int main(int argc, char **argv)
     }
     const int wg = suite == QPP_CHACHA20_POLY1305 ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
                                                   : wg_choice("QPP_WG_GCM", kGcmWG, false);
-    const int waves = (int)(((n + wg / 4 - 1) / (wg / 4)) * (wg / 64));
-    std::vector<unsigned long long> pr((size_t)waves * 16);
+#ifdef QPP_PROBE
+    std::vector<unsigned long long> pr((size_t)kProbeWaves * kProbeSlots);
+#endif
     // warm up in bench.py's order (protect, unprotect alternating)
     for (int rep = 0; rep < 3; ++rep) {
         int rc = qpp_protect(kt, d_pd, n, d_in, d_ct, d_res, nullptr);
@@ -136,6 +141,10 @@ int main(int argc, char **argv)
         hipEvent_t a, b;
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
+#ifdef QPP_PROBE
+        std::fill(pr.begin(), pr.end(), 0ull);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), pr.data(), pr.size() * 8, 0, hipMemcpyHostToDevice);
+#endif
         (void)hipEventRecord(a, nullptr);
         if (enc) (void)qpp_protect(kt, d_pd, n, d_in, d_ct, d_res, nullptr);
         else (void)qpp_unprotect(kt, d_ud, n, d_ct, d_pt, d_res, nullptr);
@@ -176,7 +185,7 @@ int main(int argc, char **argv)
                    (unsigned long long)res[i].pn, res[i].status, res[i].hdr_len, res[i].out_len);
         printf("%s: %.1f us (event), WG %d, bad %u\n", enc ? "protect" : "unprotect", ms * 1e3, wg, bad);
 #ifdef QPP_PROBE
-        report(enc ? "protect" : "unprotect", pr, waves);
+        report(enc ? "protect" : "unprotect", pr);
 #endif
     }
     return 0;
