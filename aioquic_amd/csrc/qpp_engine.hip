@@ -46,20 +46,13 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // not fit the caller's buffers: the packet reports QPP_S_LENGTH and no byte
 // of it is read or written.
 constexpr uint32_t kFlagReject = 0x8000u;
-#ifndef QPP_BALANCE
-#define QPP_BALANCE 1
-#endif
-constexpr bool kBalance = QPP_BALANCE;  // GCM wave balancing (s_setprio)
-#ifndef QPP_BALANCE_ENC
-#define QPP_BALANCE_ENC 1
-#endif
-constexpr bool kBalanceEnc = QPP_BALANCE_ENC;  // ... for protect too
-#ifndef QPP_VMCNT1
-#define QPP_VMCNT1 0  // GCM step loop: wait for the LDS-DMA only, not the last store (no gain)
-#endif
 #ifndef QPP_STORE_CPOL
 #define QPP_STORE_CPOL 0  // cache policy of the GCM step stores (gfx950: 1 sc0, 2 nt, 16 sc1)
 #endif
+#ifndef QPP_FUSE_GH
+#define QPP_FUSE_GH 0  // GCM step: GHASH product woven into the AES phases (aes_ctr_gh; measured -2.5 %)
+#endif
+constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_WPE
 #define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget)
 #endif
@@ -492,7 +485,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                                             const uint8_t *te, const Bufs &B,
                                             const uint8_t *src, uint32_t ioff, uint32_t ooff,
                                             const u32x4 hmask, const uint32_t hbits, const u32x4 h0,
-                                            uint8_t *stage, uint32_t *progress, u32x4 &got_tag)
+                                            uint8_t *stage, u32x4 &got_tag)
 {
     const LdsTe T{te, (lane_fresh() & 31) * 4};
     const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
@@ -536,11 +529,17 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     // one block of the sequence: CT block i (input `raw` loaded from CT offset
     // min(16 i, clen - 16) for protect, i.e. end-aligned for a partial tail),
     // the lengths block (i == n_c), or padding
-    auto step = [&](int i, bool last, bool first, u32x4 raw) {
+    auto step = [&](int i, bool last, auto first_c, u32x4 raw) {
+        constexpr bool first = decltype(first_c)::value;
         const bool is_ct = i >= 0 && 16 * i < clen;
         const LdsTe Tl{te, (lane_fresh() & 31) * 4};
-        (void)first;
-        const u32x4 ksb = aes_ctr<NR>(cc, is_ct ? (uint32_t)(i + 2) : 1u, rk, Tl);
+        const uint32_t cb = is_ct ? (uint32_t)(i + 2) : 1u;
+        // fused: the previous accumulator's H^4 product rides on this block's
+        // AES phases (A_k = A_{k-1} H^4 + x_k; the first step has no product)
+        u32x4 g = {0, 0, 0, 0};
+        u32x4 ksb;
+        if constexpr (!kFuseGh || first) ksb = aes_ctr<NR>(cc, cb, rk, Tl);
+        else ksb = aes_ctr_gh<NR>(cc, cb, rk, Tl, acc, G.lds, t4, g);
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
         uint32_t soff = kOob;
         if (is_ct) {
@@ -558,11 +557,15 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
         }
         __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
-        acc ^= x;
-        __builtin_amdgcn_sched_barrier(0);
-        // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
-        // is applied after the loop
-        if (!last) acc = ghash_mul_lds(acc, G.lds, t4);
+        if constexpr (kFuseGh) {
+            acc = (first ? acc : g) ^ x;
+        } else {
+            acc ^= x;
+            __builtin_amdgcn_sched_barrier(0);
+            // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
+            // is applied after the loop
+            if (!last) acc = ghash_mul_lds(acc, G.lds, t4);
+        }
     };
     // buffer offset of CT block i's input (or out of range)
     auto ct_load = [&](int i) -> uint32_t {
@@ -576,7 +579,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         QPP_PROBE_AT(4);
         // the staged bytes as an end-aligned load would see them
         const u32x4 st = *(const u32x4 *)(scr + kScrTail);
-        step(sub - q, true, true, shl_bytes(st, 16 - rlen));
+        step(sub - q, true, std::true_type{}, shl_bytes(st, 16 - rlen));
     } else {
         // LDS-DMA staging: lane l's 16 bytes land at stage[buf][16 l]
         auto dma = [&](uint32_t off, int buf) {
@@ -587,37 +590,23 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         int i = sub - q, b = 0;
         dma(ct_load(i), 0);
         QPP_PROBE_AT(4);
-        const uint32_t waves = blockDim.x >> 6;
-        uint32_t it = 0;
-        for (int k = S; k > 0; --k, i += 4, b ^= 1) {
-            // Wave balancing: issue priority goes to waves behind the
-            // workgroup's average step count (one LDS add per wave and step),
-            // so the waves finish together instead of oldest-first.
-            if (progress) {
-                const uint32_t lane = lane_fresh();
-                uint32_t old = 0;
-                if (lane == __builtin_amdgcn_readfirstlane(lane)) old = atomicAdd(progress, 1u);
-                old = __builtin_amdgcn_readfirstlane(old);
-                if (old > it * waves) __builtin_amdgcn_s_setprio(2);
-                else __builtin_amdgcn_s_setprio(0);
-                ++it;
-            }
-            // the compiler does not track LDS-DMA: retire it explicitly.  After
-            // the first step the one vector-memory op issued after this DMA is
-            // the previous step's store; gfx950 retires them in issue order,
-            // so vmcnt(1) waits for the DMA but not for that write-back
-#if QPP_VMCNT1
-            if (k == S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-#else
+        // one step: this step's input block (staged by the previous DMA), the
+        // next step's DMA, the block.  The first step is peeled (no GHASH
+        // product to weave in).
+        auto one = [&](int k, auto first_c) {
+            // the compiler does not track LDS-DMA: retire it explicitly (this
+            // also waits for the previous step's store)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
             const u32x4 raw = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
             // next step's block; on the last step the received tag
             dma((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4), b ^ 1);
-            step(i, k == 1, k == S, raw);
-        }
-        __builtin_amdgcn_s_setprio(0);
+            step(i, k == 1, first_c, raw);
+            i += 4;
+            b ^= 1;
+        };
+        one(S, std::true_type{});
+#pragma unroll 1
+        for (int k = S - 1; k > 0; --k) one(k, std::false_type{});
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
     }
@@ -1082,8 +1071,7 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
                     u32x4 got_tag;
                     const u32x4 tag = gcm_packet<kNR, ENC>(
                         P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
-                        (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0], nullptr,
-                        got_tag);
+                        (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0], got_tag);
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
                     const uint32_t t2 = tid_now(), p2 = pkt_of(t2);

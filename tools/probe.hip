@@ -58,6 +58,26 @@ static void report(const char *what, const std::vector<unsigned long long> &pr)
         e_max = std::max(e_max, (g[kProbeEnd] - t0) / 100.0);
     }
     printf("  wave ends: first %.2f us, last %.2f us\n", e_min, e_max);
+    // per workgroup (16 waves): its last wave's end, and the spread inside it
+    double g_first = 1e30, g_last = 0, spread = 0, spread_max = 0;
+    int groups = 0;
+    for (int b = 0; b < kProbeWaves / 16; ++b) {
+        double lo = 1e30, hi = 0;
+        for (int w = b * 16; w < b * 16 + 16; ++w) {
+            const unsigned long long *g = &pr[(size_t)w * kProbeSlots];
+            if (!g[kProbeStart]) continue;
+            lo = std::min(lo, (g[kProbeEnd] - t0) / 100.0);
+            hi = std::max(hi, (g[kProbeEnd] - t0) / 100.0);
+        }
+        if (hi == 0) continue;
+        ++groups;
+        g_first = std::min(g_first, hi);
+        g_last = std::max(g_last, hi);
+        spread += hi - lo;
+        spread_max = std::max(spread_max, hi - lo);
+    }
+    printf("  workgroup ends: first %.2f us, last %.2f us; wave-end spread inside a workgroup mean %.2f max %.2f us\n",
+           g_first, g_last, spread / groups, spread_max);
 }
 
 int main(int argc, char **argv)
