@@ -49,6 +49,9 @@ constexpr uint32_t kFlagReject = 0x8000u;
 #ifndef QPP_STORE_CPOL
 #define QPP_STORE_CPOL 0  // cache policy of the GCM step stores (gfx950: 1 sc0, 2 nt, 16 sc1)
 #endif
+#ifndef QPP_STAGE_LDS
+#define QPP_STAGE_LDS 0  // GCM step input: 1 = LDS-DMA staging buffers, 0 = register prefetch
+#endif
 #ifndef QPP_FUSE_GH
 #define QPP_FUSE_GH 0  // GCM step: GHASH product woven into the AES phases (aes_ctr_gh; measured -2.5 %)
 #endif
@@ -581,24 +584,25 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         const u32x4 st = *(const u32x4 *)(scr + kScrTail);
         step(sub - q, true, std::true_type{}, shl_bytes(st, 16 - rlen));
     } else {
+        int i = sub - q;
+        // one step: this step's input block, the next step's load (on the
+        // last step the received tag), the block.  The first step is peeled
+        // (no GHASH product to weave in).
+#if QPP_STAGE_LDS
         // LDS-DMA staging: lane l's 16 bytes land at stage[buf][16 l]
         auto dma = [&](uint32_t off, int buf) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 B.in, (__attribute__((address_space(3))) void *)(stage + buf * kStageBytes), 16,
                 off, 0, 0, 0);
         };
-        int i = sub - q, b = 0;
+        int b = 0;
         dma(ct_load(i), 0);
         QPP_PROBE_AT(4);
-        // one step: this step's input block (staged by the previous DMA), the
-        // next step's DMA, the block.  The first step is peeled (no GHASH
-        // product to weave in).
         auto one = [&](int k, auto first_c) {
             // the compiler does not track LDS-DMA: retire it explicitly (this
             // also waits for the previous step's store)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const u32x4 raw = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
-            // next step's block; on the last step the received tag
             dma((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4), b ^ 1);
             step(i, k == 1, first_c, raw);
             i += 4;
@@ -609,6 +613,24 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         for (int k = S - 1; k > 0; --k) one(k, std::false_type{});
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
+#else
+        // register prefetch, one step ahead (4 VGPRs; the compiler counts
+        // vmcnt, so the previous step's store stays in flight)
+        (void)stage;
+        u32x4 nxt = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i), 0, 0);
+        QPP_PROBE_AT(4);
+        auto one = [&](int k, auto first_c) {
+            const u32x4 raw = nxt;
+            nxt = __builtin_amdgcn_raw_buffer_load_b128(
+                B.in, (int)((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4)), 0, 0);
+            step(i, k == 1, first_c, raw);
+            i += 4;
+        };
+        one(S, std::true_type{});
+#pragma unroll 1
+        for (int k = S - 1; k > 0; --k) one(k, std::false_type{});
+        if (!ENC) got_tag = nxt;
+#endif
     }
     QPP_PROBE_AT(5);
     // lane-derived values recomputed after the loop rather than kept (spilled)
@@ -864,7 +886,9 @@ struct __attribute__((aligned(16))) GcmSmem {
     uint8_t h4[kTabEntries][kGhashPowBytes];  // 32 KiB
     uint8_t te[kTeBytes];                     // Te0|Te1 x 32 bank copies   64 KiB
     uint8_t scratch[WG / 4][kScratch];
+#if QPP_STAGE_LDS
     uint8_t stage[WG / 64][2][kStageBytes];   // per-wave LDS-DMA input staging
+#endif
     uint32_t eslot[kTabEntries];              // slot held by entry e (kNoSlot: none)
     uint32_t eref[kTabEntries];               // waves running entry e's slot
     uint32_t eready[kTabEntries];             // entry e's table has landed
@@ -1071,7 +1095,13 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
                     u32x4 got_tag;
                     const u32x4 tag = gcm_packet<kNR, ENC>(
                         P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
-                        (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0, sm.stage[wv][0], got_tag);
+                        (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0,
+#if QPP_STAGE_LDS
+                        sm.stage[wv][0],
+#else
+                        nullptr,
+#endif
+                        got_tag);
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
                     const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
