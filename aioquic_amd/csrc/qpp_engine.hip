@@ -57,7 +57,10 @@ constexpr uint32_t kFlagReject = 0x8000u;
 #endif
 constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_WPE
-#define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget)
+#define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget; 4: measured -2 %)
+#endif
+#ifndef QPP_CHACHA_PREFETCH
+#define QPP_CHACHA_PREFETCH 1  // ChaCha20-Poly1305: next chunk input in registers one unit ahead
 #endif
 
 template <int WG>
@@ -747,9 +750,11 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     const P130 r = p130_r(kw[0], kw[1], kw[2], kw[3]);
     if (c0 >= 0 && c0 < chunks) crypt(c0, cur, blk, x);
 
+#if QPP_CHACHA_PREFETCH
     // next unit's input, fetched one unit ahead
     u32x4 nxt[4];
     fetch(3 + sub < chunks ? 3 + sub : -1, nxt);
+#endif
 
     P130 acc = p130_zero();
     int g_last = -1;
@@ -782,9 +787,14 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     // ---- units 4k + sub, k >= 1: chunk 4k + sub - 1; later jumps skip 3 chunks (r^12)
     bool first = true;
     for (int c = 3 + sub; c < chunks; c += 4) {
+#if QPP_CHACHA_PREFETCH
 #pragma unroll
         for (int t = 0; t < 4; ++t) cur[t] = nxt[t];
         fetch(c + 4 < chunks ? c + 4 : -1, nxt);
+#else
+        // issued ahead of the block function, which hides their latency
+        fetch(c, cur);
+#endif
         chacha_block(key, (uint32_t)(1 + c), n0, n1, n2, blk);
         crypt(c, cur, blk, x);
         if (!first && g_last >= 0) acc = p130_mul(acc, r12);

@@ -1,13 +1,13 @@
 """HBM traffic per launch of the packet kernels from rocprofv3 --pmc passes.
 
-    python tools/traffic.py WORKLOAD_NAME FETCH_DIR WRITE_DIR [--out profiles/traffic.json]
+    python tools/traffic.py WORKLOAD_NAME FETCH_DIR WRITE_DIR [--packets N] [--out profiles/traffic.json]
 
-FETCH_SIZE / WRITE_SIZE are in KiB.  Corrections come from tools/calib_hbm.hip
-run on the same pool (profiles/r1_calibration.md): for the engine's pattern
-(4 lanes x 16 B contiguous per packet, LDS-DMA loads, 16 B stores, packet slots
-1200 B apart) FETCH_SIZE reads 0.597 of the bytes moved (x1.675), WRITE_SIZE
-1.035 (x0.966).  The guide's generic x2 read correction is for full 1 KiB-per-
-wave streams and overshoots this pattern.
+FETCH_SIZE / WRITE_SIZE are in KiB.  One calibration throughout, the one
+MI355X_MICROARCH.md (HBM section) prescribes for gfx950: FETCH_SIZE reports
+half the bytes of 16 B/lane streaming reads (x2), WRITE_SIZE reads the bytes
+of 16 B/lane stores exactly (x1).  (Round 1's own pattern calibration,
+tools/calib_hbm.hip, put the read factor at x1.675 for this access shape; the
+guide's factor is used so that every number in profiles/ shares one basis.)
 """
 
 import csv
@@ -16,15 +16,16 @@ import json
 import os
 import sys
 
-FETCH_CORR = 1241513984 / (723791 * 1024)   # ld_pat<false>: pattern bytes / FETCH_SIZE bytes
-WRITE_CORR = 1241513984 / (1254335 * 1024)  # st_pat<false>
+FETCH_CORR = 2.0
+WRITE_CORR = 1.0
+KERNELS = ("k_gcm", "k_chacha", "k_packets")
 
 
 def per_launch(d, counter):
     out = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter or "k_packets" not in r["Kernel_Name"]:
+            if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in KERNELS):
                 continue
             enc = "true" in r["Kernel_Name"].split("(")[0]
             out.setdefault("protect" if enc else "unprotect", []).append(float(r["Counter_Value"]))
@@ -44,7 +45,7 @@ def main():
                         "fetch_size_kib_raw": round(fetch[k] / 1024), "write_size_kib_raw": round(write[k] / 1024)}
     entry["packets"] = int(sys.argv[sys.argv.index("--packets") + 1]) if "--packets" in sys.argv else 65536
     entry["source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes ({fdir}, {wdir}); "
-                       f"corrections x{FETCH_CORR:.3f} / x{WRITE_CORR:.3f} from tools/calib_hbm.hip")
+                       f"corrections x{FETCH_CORR:g} / x{WRITE_CORR:g} (MI355X_MICROARCH.md, HBM)")
     data[name] = entry
     json.dump(data, open(dst, "w"), indent=1)
     print(json.dumps(entry, indent=1))
