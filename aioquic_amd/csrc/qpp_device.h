@@ -115,11 +115,17 @@ __device__ __forceinline__ u32x4 ld_part(const uint8_t *p, int n)
     for (int i = 0; i < n; ++i) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
     return u32x4{w[0], w[1], w[2], w[3]};
 }
+// First n (0..16) bytes of v to p: at most 4 stores (8, 4, 2, 1 bytes by the
+// bits of n), no byte loop.
 __device__ __forceinline__ void st_part(uint8_t *p, u32x4 v, int n)
 {
     if (n >= 16) { st16(p, v); return; }
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    for (int i = 0; i < n; ++i) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    uint64_t a = (uint64_t)v.y << 32 | v.x;
+    const uint64_t b = (uint64_t)v.w << 32 | v.z;
+    if (n & 8) { __builtin_memcpy(p, &a, 8); p += 8; a = b; }
+    if (n & 4) { const uint32_t w = (uint32_t)a; __builtin_memcpy(p, &w, 4); p += 4; a >>= 32; }
+    if (n & 2) { const uint16_t h = (uint16_t)a; __builtin_memcpy(p, &h, 2); p += 2; a >>= 16; }
+    if (n & 1) *p = (uint8_t)a;
 }
 // keep only the first n bytes (GHASH / Poly1305 zero padding)
 __device__ __forceinline__ u32x4 keep_bytes(u32x4 v, int n)

@@ -59,6 +59,9 @@ constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_WPE
 #define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget; 4: measured -2 %)
 #endif
+#ifndef QPP_CHACHA_ABL
+#define QPP_CHACHA_ABL 0  // ablation study only (wrong output): 1 no payload stores, 2 no payload loads, 4 no Poly1305 in the chunk loop
+#endif
 #ifndef QPP_CHACHA_PREFETCH
 #define QPP_CHACHA_PREFETCH 1  // ChaCha20-Poly1305: next chunk input in registers one unit ahead
 #endif
@@ -284,57 +287,6 @@ __device__ __forceinline__ Pkt pkt_begin(const qpp_desc &d, const HdrPre &pre, c
     return P;
 }
 
-// Protect: header protection over the finished (ct||tag) and the header write.
-template <int SUITE, class TE>
-__device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int sub,
-                                                  uint8_t *scr, u32x4 tag, const TE &T,
-                                                  const uint8_t *h0 = nullptr)
-{
-    // sample = (ct||tag)[4-pn_len : 20-pn_len]; the tag only matters when clen < 20
-    if (P.clen < 32 && sub == 0) {
-        for (int j = 0; j < 16 && P.clen + j < 32; ++j)
-            scr[P.clen + j] = (uint8_t)byte_of(tag, j);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const u32x4 sample = lds_sample(scr, 4 - P.pn_len);
-    P.mask = hp_mask_quad<SUITE>(ks, sample, T, sub);
-    const int n_a = (P.hlen + 15) >> 4;
-    for (int q = sub; q < n_a; q += 4) {
-        const int nb = min(16, P.hlen - 16 * q);
-        u32x4 h = (q == 0 && h0) ? *(const u32x4 *)h0 : ld_part(P.src + 16 * q, nb);
-        h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
-        st_part(P.dst + 16 * q, h, nb);
-    }
-}
-
-// Header out: the plain header (unprotect), or the input header with the HP
-// mask applied (protect).  Outside the step loop; byte tails allowed here.
-// h0: the input's first 16 bytes already in LDS (or null: read them).
-__device__ __forceinline__ void write_header(const Pkt &P, int sub, bool masked,
-                                             const uint8_t *h0 = nullptr)
-{
-    const int n_a = (P.hlen + 15) >> 4;
-    for (int q = sub; q < n_a; q += 4) {
-        const int nb = min(16, P.hlen - 16 * q);
-        u32x4 h = (q == 0 && h0) ? *(const u32x4 *)h0 : ld_part(P.src + 16 * q, nb);
-        if (masked) h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
-        st_part(P.dst + 16 * q, h, nb);
-    }
-}
-
-// A packet whose tag does not verify leaves no plaintext behind: its quad
-// overwrites the payload it streamed out with zeros (quic_pp.h, Authentication
-// failures).  Runs only on the failure path.  Each 16-byte block is cleared
-// by the lane that wrote it (own(i) = that lane), so the zeros land after the
-// plaintext in that lane's program order.
-template <class OWN>
-__device__ __forceinline__ void wipe_payload(const Pkt &P, int sub, OWN own)
-{
-    uint8_t *o = P.dst + P.hlen;
-    for (int i = 0; 16 * i < P.clen; ++i)
-        if (own(i) == sub) st_part(o + 16 * i, u32x4{0, 0, 0, 0}, min(16, P.clen - 16 * i));
-}
-
 // 128-bit little-endian shift right by s bytes (0..15)
 __device__ __forceinline__ u32x4 shr_bytes(u32x4 v, int s)
 {
@@ -361,6 +313,70 @@ __device__ __forceinline__ u32x4 shl_bytes(u32x4 v, int s)
         lo <<= 8 * s;
     }
     return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// n (0..16) bytes at p, zero padded, by one 16-byte load: [lo, hi) is
+// readable (a packet's region).  A block near the region's end is loaded
+// end-aligned and shifted down, so no byte loop (one memory round trip per
+// byte) runs; regions under 16 bytes take ld_part.
+__device__ __forceinline__ u32x4 ld_win(const uint8_t *p, int n, const uint8_t *lo, const uint8_t *hi)
+{
+    if (n >= 16) return ld16(p);
+    if (hi - lo < 16) return ld_part(p, n);
+    const uint8_t *a = (p + 16 <= hi) ? p : hi - 16;
+    return keep_bytes(shr_bytes(ld16(a), (int)(p - a)), n);
+}
+
+// Protect: header protection over the finished (ct||tag) and the header write.
+template <int SUITE, class TE>
+__device__ __forceinline__ void protect_finish_hp(Pkt &P, const KeySlot *ks, int sub,
+                                                  uint8_t *scr, u32x4 tag, const TE &T,
+                                                  const uint8_t *h0 = nullptr)
+{
+    // sample = (ct||tag)[4-pn_len : 20-pn_len]; the tag only matters when clen < 20
+    if (P.clen < 32 && sub == 0) {
+        for (int j = 0; j < 16 && P.clen + j < 32; ++j)
+            scr[P.clen + j] = (uint8_t)byte_of(tag, j);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const u32x4 sample = lds_sample(scr, 4 - P.pn_len);
+    P.mask = hp_mask_quad<SUITE>(ks, sample, T, sub);
+    const int n_a = (P.hlen + 15) >> 4;
+    for (int q = sub; q < n_a; q += 4) {
+        const int nb = min(16, P.hlen - 16 * q);
+        u32x4 h = (q == 0 && h0) ? *(const u32x4 *)h0 : ld_win(P.src + 16 * q, nb, P.src, P.src + P.hlen + P.clen);
+        h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
+        st_part(P.dst + 16 * q, h, nb);
+    }
+}
+
+// Header out: the plain header (unprotect), or the input header with the HP
+// mask applied (protect).  Outside the step loop; byte tails allowed here.
+// h0: the input's first 16 bytes already in LDS (or null: read them).
+// rlen: the readable input region (header + payload, + tag for unprotect).
+__device__ __forceinline__ void write_header(const Pkt &P, int sub, bool masked, int rlen,
+                                             const uint8_t *h0 = nullptr)
+{
+    const int n_a = (P.hlen + 15) >> 4;
+    for (int q = sub; q < n_a; q += 4) {
+        const int nb = min(16, P.hlen - 16 * q);
+        u32x4 h = (q == 0 && h0) ? *(const u32x4 *)h0 : ld_win(P.src + 16 * q, nb, P.src, P.src + rlen);
+        if (masked) h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
+        st_part(P.dst + 16 * q, h, nb);
+    }
+}
+
+// A packet whose tag does not verify leaves no plaintext behind: its quad
+// overwrites the payload it streamed out with zeros (quic_pp.h, Authentication
+// failures).  Runs only on the failure path.  Each 16-byte block is cleared
+// by the lane that wrote it (own(i) = that lane), so the zeros land after the
+// plaintext in that lane's program order.
+template <class OWN>
+__device__ __forceinline__ void wipe_payload(const Pkt &P, int sub, OWN own)
+{
+    uint8_t *o = P.dst + P.hlen;
+    for (int i = 0; 16 * i < P.clen; ++i)
+        if (own(i) == sub) st_part(o + 16 * i, u32x4{0, 0, 0, 0}, min(16, P.clen - 16 * i));
 }
 
 // Buffer descriptors over the whole input / output buffers.  Offsets at or
@@ -662,7 +678,7 @@ __device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, u
     if (ENC) {
         if (sub == 0) st16(P.dst + P.hlen + P.clen, tag);
         if (P.hp) protect_finish_hp<SUITE>(P, ks, sub, scr, tag, T, h0);
-        else write_header(P, sub, false, h0);
+        else write_header(P, sub, false, P.hlen + P.clen, h0);
     } else {
         const u32x4 diff = got_tag ^ tag;
         if ((diff.x | diff.y | diff.z | diff.w) != 0) {
@@ -670,7 +686,7 @@ __device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, u
             // CT block i sits at sequence position pad + za + i (gcm_packet)
             wipe_payload(P, sub, [&](int i) { return (pad + za + i) & 3; });
         }
-        write_header(P, sub, P.hp, h0);
+        write_header(P, sub, P.hp, P.hlen + P.clen + QPP_TAG_LEN, h0);
     }
 }
 
@@ -711,14 +727,20 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     const bool unmask = !ENC && P.hp;
     const uint8_t *pin = P.src + P.hlen;
     uint8_t *pout = P.dst + P.hlen;
+    // end of the readable input region (protect: header + payload; unprotect:
+    // + tag): partial blocks are loaded end-aligned within it (ld_win)
+    const int rlen = P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN);
+    // input bytes [0, 16) parked by k_chacha (absent below 16 bytes)
+    const uint8_t *h0 = rlen >= 16 ? scr + kScrHdr : nullptr;
 
     // the 64 input bytes of chunk c
     auto fetch = [&](int c, u32x4 (&v)[4]) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int i = 4 * c + t;
-            v[t] = (c >= 0 && i < n_c) ? ld_part(pin + 16 * i, min(16, P.clen - 16 * i))
-                                       : u32x4{0, 0, 0, 0};
+            v[t] = (c >= 0 && i < n_c && !(QPP_CHACHA_ABL & 2))
+                       ? ld_win(pin + 16 * i, min(16, P.clen - 16 * i), P.src, P.src + rlen)
+                       : u32x4{(uint32_t)i, 0, 0, 0};
         }
     };
     // keystream chunk c: xor, store, and the Poly1305 input blocks (ciphertext)
@@ -730,7 +752,8 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
             if (i >= n_c) continue;
             const int nb = min(16, P.clen - 16 * i);
             const u32x4 dout = din[t] ^ u32x4{blk[4 * t], blk[4 * t + 1], blk[4 * t + 2], blk[4 * t + 3]};
-            st_part(pout + 16 * i, dout, nb);
+            if (!(QPP_CHACHA_ABL & 1)) st_part(pout + 16 * i, dout, nb);
+            else if (dout.x == 0x12345678u) st16(pout, dout);
             x[t] = keep_bytes(ENC ? dout : din[t], nb);
             if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[t];
         }
@@ -762,7 +785,8 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     if (sub == 0) {
         for (int g = 0; g < n_a; ++g) {
             const int nb = min(16, P.hlen - 16 * g);
-            u32x4 a = ld_part(P.src + 16 * g, nb);
+            u32x4 a = (g == 0 && h0) ? keep_bytes(*(const u32x4 *)h0, nb)
+                                     : ld_win(P.src + 16 * g, nb, P.src, P.src + rlen);
             if (unmask) a ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
             if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
             acc = p130_mul(p130_add(acc, p130_block(a)), r);
@@ -797,12 +821,13 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
 #endif
         chacha_block(key, (uint32_t)(1 + c), n0, n1, n2, blk);
         crypt(c, cur, blk, x);
-        if (!first && g_last >= 0) acc = p130_mul(acc, r12);
+        if (!first && g_last >= 0 && !(QPP_CHACHA_ABL & 4)) acc = p130_mul(acc, r12);
         first = false;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             if (4 * c + t >= n_c) break;
-            acc = p130_mul(p130_add(acc, p130_block(x[t])), r);
+            if (!(QPP_CHACHA_ABL & 4)) acc = p130_mul(p130_add(acc, p130_block(x[t])), r);
+            else acc.v[t] ^= x[t].x;
             g_last = n_a + 4 * c + t;
         }
     }
@@ -837,7 +862,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
     const u32x4 tag = p130_finish(sum, sw.x, sw.y, sw.z, sw.w);
     if (ENC) {
         if (sub == 0) st16(pout + P.clen, tag);
-        if (P.hp) protect_finish_hp<QPP_CHACHA20_POLY1305>(P, ks, sub, scr, tag, ConstTe{});
+        if (P.hp) protect_finish_hp<QPP_CHACHA20_POLY1305>(P, ks, sub, scr, tag, ConstTe{}, h0);
     } else {
         const u32x4 got = ld16(pin + P.clen);
         const u32x4 diff = got ^ tag;
@@ -1247,7 +1272,10 @@ __global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__
             // lane-derived values from a fresh lane id: derived from t1 they
             // would be hoisted out of the loop and held live across it
             const uint32_t tf = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) << 6 | lane_fresh();
-            if (P.status == QPP_S_OK) chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2]);
+            if (P.status == QPP_S_OK) {
+                *(u32x4 *)(sm.scratch[tf >> 2] + kScrHdr) = pre.h0;
+                chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2]);
+            }
             write_result<ENC>(res, planned ? desc[p1].rsv : p1, lane_fresh() & 3, P);
         }
         last = cur;

@@ -39,7 +39,7 @@ def main(d):
             pmc[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
             meta[k] = (r["Grid_Size"], r["Workgroup_Size"], r["LDS_Block_Size"], r["VGPR_Count"],
                        r["Accum_VGPR_Count"], r["SGPR_Count"], r["Scratch_Size"])
-    kern = sorted({k for k, _ in pmc if "k_packets" in k or "k_hp_mask" in k})
+    kern = sorted({k for k, _ in pmc if any(s in k for s in ("k_packets", "k_gcm", "k_chacha", "k_hp_mask"))})
     if not kern:
         return
     print("\n## Launch resources\n")
