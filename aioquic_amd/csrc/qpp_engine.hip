@@ -59,6 +59,9 @@ constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_WPE
 #define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget; 4: measured -2 %)
 #endif
+#ifndef QPP_GCM_ABL
+#define QPP_GCM_ABL 0  // ablation study only (wrong output): step loop without 1 stores, 2 loads, 4 GHASH, 8 AES
+#endif
 #ifndef QPP_CHACHA_ABL
 #define QPP_CHACHA_ABL 0  // ablation study only (wrong output): 1 no payload stores, 2 no payload loads, 4 no Poly1305 in the chunk loop
 #endif
@@ -560,7 +563,8 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         // AES phases (A_k = A_{k-1} H^4 + x_k; the first step has no product)
         u32x4 g = {0, 0, 0, 0};
         u32x4 ksb;
-        if constexpr (!kFuseGh || first) ksb = aes_ctr<NR>(cc, cb, rk, Tl);
+        if constexpr (QPP_GCM_ABL & 8) ksb = u32x4{cb, cc.c0, cc.d0, cc.d1};
+        else if constexpr (!kFuseGh || first) ksb = aes_ctr<NR>(cc, cb, rk, Tl);
         else ksb = aes_ctr_gh<NR>(cc, cb, rk, Tl, acc, G.lds, t4, g);
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
         uint32_t soff = kOob;
@@ -578,7 +582,8 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
             *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
         }
-        __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
+        if (!(QPP_GCM_ABL & 1) || out.x == 0x12345678u)
+            __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
         if constexpr (kFuseGh) {
             acc = (first ? acc : g) ^ x;
         } else {
@@ -586,7 +591,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             __builtin_amdgcn_sched_barrier(0);
             // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
             // is applied after the loop
-            if (!last) acc = ghash_mul_lds(acc, G.lds, t4);
+            if (!last && !(QPP_GCM_ABL & 4)) acc = ghash_mul_lds(acc, G.lds, t4);
         }
     };
     // buffer offset of CT block i's input (or out of range)
@@ -640,7 +645,8 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         QPP_PROBE_AT(4);
         auto one = [&](int k, auto first_c) {
             const u32x4 raw = nxt;
-            nxt = __builtin_amdgcn_raw_buffer_load_b128(
+            if constexpr (QPP_GCM_ABL & 2) nxt = u32x4{(uint32_t)k, 0, 0, 0};
+            else nxt = __builtin_amdgcn_raw_buffer_load_b128(
                 B.in, (int)((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4)), 0, 0);
             step(i, k == 1, first_c, raw);
             i += 4;

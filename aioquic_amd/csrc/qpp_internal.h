@@ -26,7 +26,16 @@ struct qpp_plan {
     uint32_t *d_irange;          // [begin, end) of each bucket's items
     void *d_tmp;                 // rocPRIM temporary storage
     size_t tmp_bytes;
+    // Counting-sort path (tables of <= kPlanCountSlots slots): one bin per
+    // sort key, 4 << slot_bits bins.
+    uint32_t *d_bins;            // per-key counts, then the scatter cursors
+    uint32_t *d_posoff;          // first sorted position of each key's run
+    uint32_t *d_itmoff;          // first wave item of each key's run
 };
+
+// Tables up to this many slots bucket by a counting sort over (suite, slot)
+// keys; larger ones by the rocPRIM radix sort.
+constexpr uint32_t kPlanCountSlots = 4096;
 
 int qpp_internal_plan_build(qpp_plan *p, const qpp::KeySlot *d_slots, uint32_t cap,
                             const qpp_desc *d_desc, uint32_t n, hipStream_t s);

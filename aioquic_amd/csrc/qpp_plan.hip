@@ -10,6 +10,8 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
+#include <stdlib.h>
+
 #include "qpp_internal.h"
 
 namespace qpp {
@@ -103,6 +105,158 @@ __global__ void k_plan_iranges(const uint32_t *__restrict__ range, const uint32_
     irange[threadIdx.x] = r < n ? pos[r] : *total;
 }
 
+// ---- counting-sort path (tables of <= kPlanCountSlots slots) -------------
+//
+// keys -> per-key counts (bins) -> one-workgroup scan of the bins (each key's
+// first position and first wave item; bucket ranges) -> wave items -> each
+// packet's position: its rank within its workgroup's packets of that key plus
+// the range the workgroup took from the key's cursor.
+// Packets of one key keep no particular order among themselves (the results
+// go back to the caller's order through rsv, so the order is not observable).
+
+constexpr int kScanWG = 1024;
+constexpr uint32_t kMaxBins = 4u << 12;  // 4 buckets x 4096 slots (kPlanCountSlots)
+
+__device__ __forceinline__ uint32_t plan_key(const KeySlot *slots, uint32_t cap, uint32_t s, int slot_bits)
+{
+    uint32_t b = kNoKeyBucket;
+    if (s < cap) {
+        const uint32_t suite = slots[s].suite;
+        if (suite <= QPP_CHACHA20_POLY1305) b = suite;
+    }
+    return b << slot_bits | (s < cap ? s : 0u);
+}
+
+// Per-key counts: a workgroup of kScanWG packets counts its keys in an LDS
+// histogram, then adds each non-zero bin to the global one (a batch on one
+// connection would otherwise serialize its atomics on one address).
+__global__ __launch_bounds__(kScanWG) void k_cnt_keys(const KeySlot *__restrict__ slots, uint32_t cap,
+                                                      const qpp_desc *__restrict__ desc, uint32_t n,
+                                                      int slot_bits, uint32_t nb, uint32_t *__restrict__ keys,
+                                                      uint32_t *__restrict__ bins)
+{
+    __shared__ uint32_t h[kMaxBins];
+    for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) h[b] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kScanWG + threadIdx.x;
+    if (i < n) {
+        const uint32_t k = plan_key(slots, cap, desc[i].slot, slot_bits);
+        keys[i] = k;
+        atomicAdd(&h[k], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += kScanWG)
+        if (h[b]) atomicAdd(&bins[b], h[b]);
+}
+
+// One workgroup: bins[nb] counts -> posoff / itmoff (exclusive scans of the
+// counts and of their wave items), bins[] = posoff (the scatter cursors),
+// range / irange per bucket, count[24] = wave items in all, items[total] = n.
+__global__ __launch_bounds__(kScanWG) void k_cnt_scan(uint32_t *__restrict__ bins, uint32_t nb, int slot_bits,
+                                                      uint32_t n, uint32_t *__restrict__ posoff,
+                                                      uint32_t *__restrict__ itmoff,
+                                                      uint32_t *__restrict__ count, uint32_t *__restrict__ items)
+{
+    __shared__ uint32_t c[kMaxBins];
+    __shared__ uint32_t sp[kScanWG], si[kScanWG];
+    for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) c[b] = bins[b];
+    __syncthreads();
+    const uint32_t per = (nb + kScanWG - 1) / kScanWG, b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    uint32_t tp = 0, ti = 0;
+    for (uint32_t b = b0; b < b1; ++b) {
+        tp += c[b];
+        ti += (c[b] + kItemPackets - 1) / kItemPackets;
+    }
+    sp[threadIdx.x] = tp;
+    si[threadIdx.x] = ti;
+    __syncthreads();
+    // inclusive Hillis-Steele scan of the per-thread sums
+    for (int d = 1; d < kScanWG; d <<= 1) {
+        const uint32_t ap = threadIdx.x >= (uint32_t)d ? sp[threadIdx.x - d] : 0u;
+        const uint32_t ai = threadIdx.x >= (uint32_t)d ? si[threadIdx.x - d] : 0u;
+        __syncthreads();
+        sp[threadIdx.x] += ap;
+        si[threadIdx.x] += ai;
+        __syncthreads();
+    }
+    uint32_t pos = sp[threadIdx.x] - tp, itm = si[threadIdx.x] - ti;
+    const uint32_t total = si[kScanWG - 1];
+    const uint32_t smask = (1u << slot_bits) - 1;
+    for (uint32_t b = b0; b < b1; ++b) {
+        if ((b & smask) == 0) {
+            // first bin of bucket b >> slot_bits: the bucket's start, the previous bucket's end
+            const uint32_t s = b >> slot_bits;
+            count[8 + 2 * s] = pos;
+            count[16 + 2 * s] = itm;
+            if (s > 0) {
+                count[8 + 2 * s - 1] = pos;
+                count[16 + 2 * s - 1] = itm;
+            }
+        }
+        posoff[b] = pos;
+        itmoff[b] = itm;
+        bins[b] = pos;
+        pos += c[b];
+        itm += (c[b] + kItemPackets - 1) / kItemPackets;
+    }
+    if (threadIdx.x == 0) {
+        count[8 + 7] = n;
+        count[16 + 7] = total;
+        count[24] = total;
+        items[total] = n;
+    }
+}
+
+// items[j] = first sorted position of wave item j (j < total)
+__global__ __launch_bounds__(kPlanWG) void k_cnt_items(const uint32_t *__restrict__ posoff,
+                                                       const uint32_t *__restrict__ itmoff, uint32_t nb,
+                                                       const uint32_t *__restrict__ count,
+                                                       uint32_t *__restrict__ items)
+{
+    const uint32_t j = blockIdx.x * kPlanWG + threadIdx.x;
+    if (j >= count[24]) return;
+    // the last bin whose first item is <= j holds item j
+    uint32_t lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (itmoff[mid] <= j) lo = mid;
+        else hi = mid - 1;
+    }
+    items[j] = posoff[lo] + kItemPackets * (j - itmoff[lo]);
+}
+
+// idx[position] = caller index.  Each workgroup ranks its packets per key in
+// LDS, takes one range per non-zero key from the key's cursor (one global
+// atomic per key and workgroup, all in flight together), and scatters.
+__global__ __launch_bounds__(kScanWG) void k_cnt_scatter(const uint32_t *__restrict__ keys, uint32_t n,
+                                                         uint32_t nb, uint32_t *__restrict__ cursor,
+                                                         uint32_t *__restrict__ idx)
+{
+    constexpr int kPer = kMaxBins / kScanWG;  // bins per thread
+    __shared__ uint32_t h[kMaxBins];
+    for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) h[b] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kScanWG + threadIdx.x;
+    const uint32_t k = i < n ? keys[i] : 0u;
+    const uint32_t r = i < n ? atomicAdd(&h[k], 1u) : 0u;
+    __syncthreads();
+    uint32_t base[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const uint32_t b = threadIdx.x + u * kScanWG;
+        const uint32_t c = b < nb ? h[b] : 0u;
+        base[u] = c ? atomicAdd(&cursor[b], c) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const uint32_t b = threadIdx.x + u * kScanWG;
+        if (b < nb) h[b] = base[u];
+    }
+    __syncthreads();
+    if (i < n) idx[h[k] + r] = i;
+}
+
 // sorted[p] = desc[idx[p]], with the caller's index in rsv
 __global__ __launch_bounds__(kPlanWG) void k_plan_gather(const qpp_desc *__restrict__ desc,
                                                          const uint32_t *__restrict__ idx, uint32_t n,
@@ -153,7 +307,9 @@ extern "C" int qpp_plan_create(uint32_t max_packets, qpp_plan **out)
               hipMalloc(&p->d_sorted, n * sizeof(qpp_desc)) == hipSuccess &&
               hipMalloc(&p->d_flags, n * 4) == hipSuccess && hipMalloc(&p->d_pos, n * 4) == hipSuccess &&
               hipMalloc(&p->d_items, (n + 1) * 4) == hipSuccess &&
-              hipMalloc(&p->d_count, 32 * sizeof(uint32_t)) == hipSuccess;
+              hipMalloc(&p->d_count, 32 * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&p->d_bins, kMaxBins * 4) == hipSuccess && hipMalloc(&p->d_posoff, kMaxBins * 4) == hipSuccess &&
+              hipMalloc(&p->d_itmoff, kMaxBins * 4) == hipSuccess;
     if (ok) {
         size_t tmp = 0, tmp2 = 0;
         ok = rocprim::radix_sort_pairs(nullptr, tmp, p->d_keys[0], p->d_keys[1], p->d_idx[0], p->d_idx[1],
@@ -188,6 +344,9 @@ extern "C" void qpp_plan_destroy(qpp_plan *p)
     if (p->d_pos) (void)hipFree(p->d_pos);
     if (p->d_items) (void)hipFree(p->d_items);
     if (p->d_tmp) (void)hipFree(p->d_tmp);
+    if (p->d_bins) (void)hipFree(p->d_bins);
+    if (p->d_posoff) (void)hipFree(p->d_posoff);
+    if (p->d_itmoff) (void)hipFree(p->d_itmoff);
     free(p);
 }
 
@@ -198,6 +357,22 @@ int qpp_internal_plan_build(qpp_plan *p, const KeySlot *d_slots, uint32_t cap, c
     if (hipMemsetAsync(p->d_count, 0, 32 * sizeof(uint32_t), s) != hipSuccess) return QPP_E_HIP;
     const int sb = bits_for(cap);
     const dim3 grid((n + kPlanWG - 1) / kPlanWG);
+    if (n && cap <= kPlanCountSlots && getenv("QPP_PLAN_RADIX") == nullptr) {
+        const uint32_t nb = 4u << sb;
+        if (hipMemsetAsync(p->d_bins, 0, nb * 4, s) != hipSuccess) return QPP_E_HIP;
+        const dim3 cgrid((n + kScanWG - 1) / kScanWG);
+        hipLaunchKernelGGL(k_cnt_keys, cgrid, dim3(kScanWG), 0, s, d_slots, cap, d_desc, n, sb, nb, p->d_keys[0],
+                           p->d_bins);
+        hipLaunchKernelGGL(k_cnt_scan, dim3(1), dim3(kScanWG), 0, s, p->d_bins, nb, sb, n, p->d_posoff,
+                           p->d_itmoff, p->d_count, p->d_items);
+        const uint32_t mi = qpp_internal_plan_max_items(n, cap);
+        hipLaunchKernelGGL(k_cnt_items, dim3((mi + kPlanWG - 1) / kPlanWG), dim3(kPlanWG), 0, s, p->d_posoff,
+                           p->d_itmoff, nb, p->d_count, p->d_items);
+        hipLaunchKernelGGL(k_cnt_scatter, cgrid, dim3(kScanWG), 0, s, p->d_keys[0], n, nb, p->d_bins, p->d_idx[1]);
+        if (hipGetLastError() != hipSuccess) return QPP_E_HIP;
+        p->n_built = n;
+        return QPP_OK;
+    }
     if (n) {
         hipLaunchKernelGGL(k_plan_keys, grid, dim3(kPlanWG), 0, s, d_slots, cap, d_desc, n, sb, p->d_keys[0],
                            p->d_idx[0], p->d_count);

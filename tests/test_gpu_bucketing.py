@@ -62,7 +62,18 @@ def _run(eng, fn_name, desc, n, inbuf, out_size, plan):
     return d_out.cpu().numpy(), d_res.cpu().numpy().view(L.RESULT)
 
 
-def test_planned_equals_unplanned_and_oracle(oracle):
+@pytest.fixture(params=["counting", "radix"])
+def plan_path(request, monkeypatch):
+    """Both bucketing paths: the counting sort (tables of <= 4096 slots) and
+    the rocPRIM radix sort (larger tables; forced by QPP_PLAN_RADIX)."""
+    if request.param == "radix":
+        monkeypatch.setenv("QPP_PLAN_RADIX", "1")
+    else:
+        monkeypatch.delenv("QPP_PLAN_RADIX", raising=False)
+    return request.param
+
+
+def test_planned_equals_unplanned_and_oracle(oracle, plan_path):
     """A random ragged batch over all suites, interleaved slots, some of them
     empty or out of range: the planned path gives the same bytes and results
     as the unplanned one and the oracle, in the caller's order."""
@@ -113,7 +124,7 @@ def test_planned_equals_unplanned_and_oracle(oracle):
         assert back_p[o : o + len(headers[i]) + len(payloads[i])].tobytes() == headers[i] + payloads[i]
 
 
-def test_wave_items_ragged_runs(oracle):
+def test_wave_items_ragged_runs(oracle, plan_path):
     """Key runs of 1, 15, 16, 17, 31, 33, 64, 255 and 257 packets (the plan's
     wave items split them at 16), all suites, shuffled arrival: planned ==
     unplanned == oracle for every packet."""
