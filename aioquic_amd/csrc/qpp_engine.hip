@@ -65,12 +65,27 @@ constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_ABL
 #define QPP_CHACHA_ABL 0  // ablation study only (wrong output): 1 no payload stores, 2 no payload loads, 4 no Poly1305 in the chunk loop
 #endif
+#ifndef QPP_CHACHA_STAGE
+#define QPP_CHACHA_STAGE 1  // ChaCha20-Poly1305: coalesced loads / stores through LDS staging (0: per-lane chunks)
+#endif
 #ifndef QPP_CHACHA_PREFETCH
 #define QPP_CHACHA_PREFETCH 1  // ChaCha20-Poly1305: next chunk input in registers one unit ahead
 #endif
 
+// ChaCha20-Poly1305 per-wave LDS staging: at step k a quad works on 4
+// consecutive 64-byte chunks of its packet (lane j: chunk 4k - 1 + j).  Its
+// loads and stores run coalesced, chunk by chunk (instruction t: lane j moves
+// 16-byte block j of chunk 4k - 1 + t), through 4 regions of 64 x 16 bytes
+// (region t: instruction t's LDS-DMA destination / store source), each padded
+// by 16 bytes so that a quad's 4 lanes reading one chunk hit distinct banks.
+constexpr int kChRegion = 64 * 16 + 16;
+constexpr int kChStage = 4 * kChRegion;
+
 template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
+#if QPP_CHACHA_STAGE
+    uint8_t stage[WG / 64][kChStage];
+#endif
     uint8_t scratch[WG / 4][kScratch];
 };
 
@@ -722,6 +737,173 @@ __device__ __forceinline__ P130 launder(P130 x)
     return x;
 }
 
+#if QPP_CHACHA_STAGE
+// 16 bytes per lane from buffer offset `off` (out of range: zeros) into LDS at
+// lds + 16 * lane (LDS-DMA)
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds, uint32_t off)
+{
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)lds, 16, off, 0, 0,
+                                             0);
+}
+
+// Work of a packet's quad, staged form (RFC 8439 sec. 2.8; _crypto.c:157-204
+// / :115-155).  Unit u = ChaCha20 block counter u: u = 0 is the Poly1305 key
+// block (RFC 8439 sec. 2.6), u >= 1 encrypts 64-byte chunk u - 1.  Lane j
+// runs unit 4k + j at step k, so a quad's step covers chunks 4k - 1 .. 4k + 2,
+// 256 contiguous payload bytes, moved by 4 coalesced LDS-DMA loads and 4
+// coalesced stores (kChRegion).  Poly1305 is per-lane Horner over the lane's
+// chunks (r per block, r^12 across the other 3 lanes' chunks), lane 0 starting
+// with the associated data, and one quad sum at the end.  B / ioff / ooff:
+// the wave's buffer views and the packet's offsets in them.
+template <bool ENC>
+__device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, uint8_t *stage,
+                              const Bufs &B, uint32_t ioff, uint32_t ooff)
+{
+    const uint32_t *key = ks->rk;
+    const uint32_t n0 = P.nonce.x, n1 = P.nonce.y, n2 = P.nonce.z;
+    const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4;
+    const int n_g = n_a + n_c + 1;
+    const int chunks = (P.clen + 63) >> 6;
+    const bool unmask = !ENC && P.hp;
+    const uint8_t *pin = P.src + P.hlen;
+    uint8_t *pout = P.dst + P.hlen;
+    const int rlen = P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN);
+    // < 16 readable bytes (AEAD-only protect of a short input): byte loads
+    const bool tiny = rlen < 16;
+    const uint8_t *h0 = tiny ? nullptr : scr + kScrHdr;
+    const int steps = (chunks + 4) >> 2;  // units 0..chunks, 4 per step
+    // payload block i: its 16 input bytes, end-aligned within the region for
+    // a protect's partial last block (the consumer shifts it down)
+    auto blk_off = [&](int i) -> uint32_t {
+        if (i < 0 || i >= n_c || tiny) return kOob;
+        const int o = P.hlen + 16 * i;
+        return ioff + (uint32_t)(ENC ? min(o, rlen - 16) : o);
+    };
+    // LDS-DMA of step k's 4 chunks: instruction t, lane j -> block j of chunk 4k - 1 + t
+    auto dma = [&](int k) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) lds_dma16(B.in, stage + t * kChRegion, blk_off(4 * (4 * k - 1 + t) + sub));
+    };
+    const uint32_t qoff = (lane_fresh() >> 2) * 64;  // the quad's 64 bytes in each region
+
+    dma(0);
+    P130 acc = p130_zero(), r = p130_zero(), r12 = p130_zero();
+    int g_last = -1;
+#pragma unroll 1
+    for (int k = 0; k < steps; ++k) {
+        const int c = 4 * k + sub - 1;  // this lane's chunk (-1: the key block)
+        uint32_t blk[16];
+        chacha_block(key, (uint32_t)(c + 1), n0, n1, n2, blk);
+        if (k == 0) {
+            // one-time key from lane 0: r, and s parked in LDS until the tag
+            uint32_t kw[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) kw[w] = quad_dpp<0x00>(blk[w]);
+            *(u32x4 *)(scr + 64) = u32x4{kw[4], kw[5], kw[6], kw[7]};
+            r = p130_r(kw[0], kw[1], kw[2], kw[3]);
+            const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2);
+            r12 = p130_mul(p130_mul(r4, r4), r4);
+            // lane 0 starts its chain with the associated data
+            if (sub == 0) {
+                for (int g = 0; g < n_a; ++g) {
+                    const int nb = min(16, P.hlen - 16 * g);
+                    u32x4 a = (g == 0 && h0) ? keep_bytes(*(const u32x4 *)h0, nb)
+                                             : ld_win(P.src + 16 * g, nb, P.src, P.src + rlen);
+                    if (unmask) a ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
+                    if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
+                    acc = p130_mul(p130_add(acc, p130_block(a)), r);
+                    g_last = g;
+                }
+            }
+        }
+        // the lane's chunk from region `sub` (the DMA retires in issue order,
+        // after the previous step's stores: vmcnt(0) waits for both)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint8_t *mine = stage + sub * kChRegion + qoff;
+        u32x4 x[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int i = 4 * c + b;
+            const bool valid = c >= 0 && i < n_c;
+            const int nb = min(16, P.clen - 16 * i);
+            u32x4 in = *(const u32x4 *)(mine + 16 * b);
+            if (tiny) in = valid ? ld_part(pin + 16 * i, nb) : in;
+            else if (ENC && nb < 16) in = shr_bytes(in, 16 - nb);
+            const u32x4 o = in ^ u32x4{blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3]};
+            x[b] = u32x4{0, 0, 0, 0};
+            if (valid) {
+                x[b] = keep_bytes(ENC ? o : in, nb);
+                if (nb < 16) st_part(pout + 16 * i, o, nb);  // partial block: byte-exact, direct
+                if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[b];
+            }
+            *(u32x4 *)(mine + 16 * b) = o;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // coalesced stores of the quad's full blocks: instruction t, lane j ->
+        // block j of chunk 4k - 1 + t
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i = 4 * (4 * k - 1 + t) + sub;
+            const uint32_t so = (i >= 0 && 16 * i + 16 <= P.clen && !tiny) ? ooff + (uint32_t)(P.hlen + 16 * i) : kOob;
+            const u32x4 v = *(const u32x4 *)(stage + t * kChRegion + qoff + 16 * sub);
+            __builtin_amdgcn_raw_buffer_store_b128(v, B.out, (int)so, 0, 0);
+        }
+        // the regions are read: next step's input (hidden behind this step's
+        // Poly1305 and the next ChaCha20 block)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (k + 1 < steps) dma(k + 1);
+        if (c >= 0 && c < chunks) {
+            if (g_last >= 0) acc = p130_mul(acc, r12);  // the 3 other lanes' chunks (12 blocks)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                if (4 * c + b >= n_c) break;
+                acc = p130_mul(p130_add(acc, p130_block(x[b])), r);
+                g_last = n_a + 4 * c + b;
+            }
+        }
+    }
+    // acc = sum m_g r^(g_last - g + 1); scale to r^(n_g - g) with r^(n_g - 1 - g_last)
+    int e = n_g - 1 - g_last;
+    if (g_last < 0) e = 0;
+    P130 f = acc;
+    if (e > 1) {
+        const P130 rr = launder(r);
+        const P130 r2 = p130_mul(rr, rr), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
+        const int m = e - 1;
+        if (m & 1) f = p130_mul(f, rr);
+        if (m & 2) f = p130_mul(f, r2);
+        if (m & 4) f = p130_mul(f, r4);
+        if (m & 8) f = p130_mul(f, r8);
+        if (m & 16) f = p130_mul(f, p130_mul(r8, r8));
+    }
+    P130 sum;
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        uint32_t v = f.v[l];
+        v += quad_perm<kQuadSwap1>(v);
+        v += quad_perm<kQuadSwap2>(v);
+        sum.v[l] = v;
+    }
+    const u32x4 lens = u32x4{(uint32_t)P.hlen, 0u, (uint32_t)P.clen, 0u};
+    sum = p130_mul(p130_add(sum, p130_block(lens)), r);
+    const u32x4 sw = *(const u32x4 *)(scr + 64);
+    const u32x4 tag = p130_finish(sum, sw.x, sw.y, sw.z, sw.w);
+    if (ENC) {
+        if (sub == 0) st16(pout + P.clen, tag);
+        if (P.hp) protect_finish_hp<QPP_CHACHA20_POLY1305>(P, ks, sub, scr, tag, ConstTe{}, h0);
+    } else {
+        const u32x4 got = ld16(pin + P.clen);
+        const u32x4 diff = got ^ tag;
+        if ((diff.x | diff.y | diff.z | diff.w) != 0) {
+            P.status = QPP_S_DECRYPT;
+            // chunk c (blocks 4c..4c+3) is unit c + 1, run by lane (c + 1) & 3
+            wipe_payload(P, sub, [&](int i) { return ((i >> 2) + 1) & 3; });
+        }
+    }
+}
+#else
 template <bool ENC>
 __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
 {
@@ -879,6 +1061,8 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
         }
     }
 }
+
+#endif  // QPP_CHACHA_STAGE
 
 template <bool ENC>
 __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int sub, const Pkt &P)
@@ -1250,9 +1434,26 @@ __global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__
     const uint32_t lim = W.e, planned = irange != nullptr;
     __shared__ ChachaSmem<WG> sm;
     const uint32_t t1 = threadIdx.x, p1 = W.b + ((t1 & 63) >> 2);
-    if (p1 < lim && (t1 & 3) == 0) {
-        const qpp_desc d = desc[p1];
-        if (d.slot >= cap) res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+#if QPP_CHACHA_STAGE
+    // 32-bit buffer views based at the wave's lowest input / output offsets
+    // (a wave's packets must lie within 4 GiB of each other, as for GCM)
+    uint64_t bi, bo;
+#endif
+    {
+        uint64_t in0 = ~0ull, out0 = ~0ull;
+        if (p1 < lim) {
+            const qpp_desc d = desc[p1];
+            in0 = d.in_off;
+            out0 = d.out_off;
+            if (d.slot >= cap && (t1 & 3) == 0) res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+        }
+#if QPP_CHACHA_STAGE
+        bi = wave_min_u64(in0);
+        bo = wave_min_u64(out0);
+#else
+        (void)in0;
+        (void)out0;
+#endif
     }
     // slot by slot among the wave's packets, lowest first (usually one); the
     // descriptor is re-read each time rather than kept live (VGPRs)
@@ -1278,9 +1479,24 @@ __global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__
             // lane-derived values from a fresh lane id: derived from t1 they
             // would be hoisted out of the loop and held live across it
             const uint32_t tf = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) << 6 | lane_fresh();
+#if QPP_CHACHA_STAGE
+            const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
+            if (P.status == QPP_S_OK &&
+                (ioff + (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN) > kBufBytes ||
+                 ooff + (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN) > kBufBytes))
+                P.status = QPP_S_LENGTH;  // the wave's packets span more than 4 GiB
+#endif
             if (P.status == QPP_S_OK) {
                 *(u32x4 *)(sm.scratch[tf >> 2] + kScrHdr) = pre.h0;
+#if QPP_CHACHA_STAGE
+                const Bufs B{
+                    __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
+                    __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
+                chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2], sm.stage[tf >> 6], B, (uint32_t)ioff,
+                                   (uint32_t)ooff);
+#else
                 chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2]);
+#endif
             }
             write_result<ENC>(res, planned ? desc[p1].rsv : p1, lane_fresh() & 3, P);
         }
