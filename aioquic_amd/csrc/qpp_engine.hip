@@ -59,6 +59,9 @@ constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_WPE
 #define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget; 4: measured -2 %)
 #endif
+#ifndef QPP_GCM_PF
+#define QPP_GCM_PF 1  // GCM step input: register prefetch distance in steps (1, or 2: same time on 1Mi and config 4, +6 VGPRs)
+#endif
 #ifndef QPP_GCM_ABL
 #define QPP_GCM_ABL 0  // ablation study only (wrong output): step loop without 1 stores, 2 loads, 4 GHASH, 8 AES
 #endif
@@ -656,13 +659,28 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         // register prefetch, one step ahead (4 VGPRs; the compiler counts
         // vmcnt, so the previous step's store stays in flight)
         (void)stage;
+        // the input of the step after step k (counting down to 1; step 0 is
+        // the received tag of an unprotect), block j = i + 4 (S - k)
+        auto in_of = [&](int k, int j) -> uint32_t {
+            return (!ENC && k == 0) ? cin + (uint32_t)clen : ct_load(j);
+        };
         u32x4 nxt = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i), 0, 0);
+#if QPP_GCM_PF >= 2
+        // two steps ahead: a step's LDS work (~3 us per wave at 16 waves/CU)
+        // is shorter than a loaded HBM read
+        u32x4 nxt2 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)in_of(S - 1, i + 4), 0, 0);
+#endif
         QPP_PROBE_AT(4);
         auto one = [&](int k, auto first_c) {
             const u32x4 raw = nxt;
+#if QPP_GCM_PF >= 2
+            nxt = nxt2;
+            if constexpr (QPP_GCM_ABL & 2) nxt2 = u32x4{(uint32_t)k, 0, 0, 0};
+            else nxt2 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)(k >= 2 ? in_of(k - 2, i + 8) : kOob), 0, 0);
+#else
             if constexpr (QPP_GCM_ABL & 2) nxt = u32x4{(uint32_t)k, 0, 0, 0};
-            else nxt = __builtin_amdgcn_raw_buffer_load_b128(
-                B.in, (int)((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4)), 0, 0);
+            else nxt = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)in_of(k - 1, i + 4), 0, 0);
+#endif
             step(i, k == 1, first_c, raw);
             i += 4;
         };
