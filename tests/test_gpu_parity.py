@@ -275,17 +275,19 @@ def test_aead_only_batch(oracle, L, engine_cls):
         assert np.array_equal(u[o : o + ln], uo[o : o + ln]), i
 
 
-def test_full_size_round_trip_64k(L, engine_cls):
-    """BASELINE config 2 shape on device tensors: 64Ki x 1200 B, AES-128-GCM,
-    one key.  Size-independent properties: round trip identity, all tags
-    verify, every ciphertext differs from its plaintext, and a checksum of the
-    protected batch against the oracle on a sampled subset."""
+@pytest.mark.parametrize("suite,version", [(0, 1), (2, 0x6B3343CF)], ids=["config2-aes128", "config3-chacha-v2"])
+def test_full_size_round_trip_64k(L, engine_cls, suite, version):
+    """BASELINE configs 2 and 3 on device tensors: 64Ki x 1200 B, one key,
+    AES-128-GCM (QUIC v1) or ChaCha20-Poly1305 (QUIC v2 labels).
+    Size-independent properties: round trip identity, all tags verify, every
+    ciphertext differs from its plaintext, and the protected bytes against the
+    oracle on a sampled subset."""
     import torch
 
     from aioquic_amd import bench_data
 
     n = 65536
-    w = bench_data.make_workload(n, suite=0, n_keys=1, seed=0x9002)
+    w = bench_data.make_workload(n, suite=suite, n_keys=1, seed=0x9002, version=version)
     eng = engine_cls(w.n_keys)
     eng.set_key_records(w.keys)
     dev = torch.device("cuda")
