@@ -422,6 +422,68 @@ __device__ __forceinline__ u32x4 aes_ctr(const CtrCache &c, uint32_t cb, const u
     return aes_rounds<NR, 3, true>(v, rk, T);
 }
 
+// Two counter blocks of one packet (cb0, cb1) as one chain of LDS phases:
+// every phase issues both blocks' lookups (32 for a full round) before the
+// first use, so a block pays half the LDS round trips of aes_ctr.
+template <int NR, class TE>
+__device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32_t cb1,
+                                         const uint32_t *rk, const TE &T, u32x4 &o0, u32x4 &o1)
+{
+    const uint32_t x0 = T.t3(rk[3] ^ (cb0 << 24)), x1 = T.t3(rk[3] ^ (cb1 << 24));
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t u0 = c.c0 ^ x0, u1 = c.c0 ^ x1;
+    const uint32_t v0 = T.t0(u0), v1 = T.t3(u0), v2 = T.t2(u0), v3 = T.t1(u0);
+    const uint32_t w0 = T.t0(u1), w1 = T.t3(u1), w2 = T.t2(u1), w3 = T.t1(u1);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t s[2][4] = {{c.d0 ^ v0, c.d1 ^ v1, c.d2 ^ v2, c.d3 ^ v3},
+                        {c.d0 ^ w0, c.d1 ^ w1, c.d2 ^ w2, c.d3 ^ w3}};
+#pragma unroll
+    for (int r = 3; r < NR; ++r) {
+        const uint32_t *k = rk + 4 * r;
+        uint32_t e[2][16];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+#pragma unroll
+            for (int col = 0; col < 4; ++col) {
+                e[b][4 * col + 0] = T.t0(s[b][col]);
+                e[b][4 * col + 1] = T.t1(s[b][(col + 1) & 3]);
+                e[b][4 * col + 2] = T.t2r(s[b][(col + 2) & 3]);
+                e[b][4 * col + 3] = T.t3r(s[b][(col + 3) & 3]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+#pragma unroll
+            for (int col = 0; col < 4; ++col)
+                s[b][col] = xor3(e[b][4 * col], e[b][4 * col + 1],
+                                 rotl(xor3(e[b][4 * col + 2], e[b][4 * col + 3], k[col]), 16));
+        }
+    }
+    const uint32_t *k = rk + 4 * NR;
+    uint32_t f[2][16];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int col = 0; col < 4; ++col) {
+            f[b][4 * col + 0] = T.f0(s[b][col]);
+            f[b][4 * col + 1] = T.f1(s[b][(col + 1) & 3]);
+            f[b][4 * col + 2] = T.f2(s[b][(col + 2) & 3]);
+            f[b][4 * col + 3] = T.f3(s[b][(col + 3) & 3]);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t o[2][4];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int col = 0; col < 4; ++col)
+            o[b][col] = (f[b][4 * col] | f[b][4 * col + 1] | f[b][4 * col + 2] | f[b][4 * col + 3]) ^ k[col];
+    }
+    o0 = u32x4{o[0][0], o[0][1], o[0][2], o[0][3]};
+    o1 = u32x4{o[1][0], o[1][1], o[1][2], o[1][3]};
+}
+
 // --------------------------------------------------------------- GHASH ----
 
 // One window pair of a GHASH product (see ghash_mul): windows 2j (low nibble)

@@ -57,7 +57,7 @@ constexpr uint32_t kFlagReject = 0x8000u;
 #endif
 constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_WPE
-#define QPP_CHACHA_WPE 1  // ChaCha20-Poly1305: minimum waves per SIMD (VGPR budget; 4: measured -2 %)
+#define QPP_CHACHA_WPE 4  // ChaCha20-Poly1305: minimum waves per SIMD (4: 128 VGPRs, 8 spilled; r2i same box vs 1 (146 VGPRs, 3 waves): 64Ki +4 %, 1Mi +1 %, config 5 +1 %)
 #endif
 #ifndef QPP_GCM_PF
 #define QPP_GCM_PF 1  // GCM step input: register prefetch distance in steps (1, or 2: same time on 1Mi and config 4, +6 VGPRs)
@@ -521,7 +521,18 @@ struct GhashTabs {
     }
 };
 
-template <int NR, bool ENC>
+// Sequence positions per quad step: BPL blocks per lane.  Lane j owns the
+// positions v = j (mod 4) in either form; with BPL = 2 a step covers two of
+// them (8 contiguous blocks per quad: two AES chains per lane in one set of
+// LDS round trips, and 128 contiguous output bytes per quad step).
+template <int BPL>
+__device__ __forceinline__ int gcm_pad(int n_g)
+{
+    constexpr int QS = 4 * BPL;
+    return QS * ((n_g + QS - 1) / QS) - n_g;
+}
+
+template <int NR, bool ENC, int BPL>
 __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int clen,
                                             const uint32_t *rk, int sub, uint8_t *scr,
                                             uint8_t *scr_wave, const GhashTabs &G,
@@ -532,7 +543,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
 {
     const LdsTe T{te, (lane_fresh() & 31) * 4};
     const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
-    const int n_g = za + n_c + 1, S = (n_g + 3) >> 2, pad = 4 * S - n_g;
+    const int n_g = za + n_c + 1, pad = gcm_pad<BPL>(n_g), S = (n_g + pad) / (4 * BPL);
     const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
     const bool tiny = rlen < 16;
     // the H^4 entry, read once: an LDS read inside the step loop would make
@@ -561,7 +572,10 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         if (g > 0) z = ghash_mul_global(z, G.global(0));  // H^1
         z ^= a;
     }
-    u32x4 acc = (za && sub == pad) ? z : u32x4{0, 0, 0, 0};
+    // BPL = 1: Z enters as lane `pad`'s initial accumulator (position pad is
+    // in its first step's only block); BPL = 2: Z may sit at the second block
+    // of a lane's first step, so it enters through that step's input (step2)
+    u32x4 acc = (BPL == 1 && za && sub == pad) ? z : u32x4{0, 0, 0, 0};
     const int q = pad + za;  // sequence position of CT block 0
     // E_K(J0) slot starts at zero: lanes other than the lengths lane add 0
     *(u32x4 *)(scr + kScrEj0) = zero4();
@@ -617,9 +631,98 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         if (i < 0 || 16 * i >= clen) return kOob;
         return cin + (uint32_t)(ENC ? min(16 * i, clen - 16) : 16 * i);
     };
+    // BPL = 2: the output side of one block (as in `step`) given its keystream;
+    // returns the GHASH input of the block
+    auto blk_out = [&](int i, u32x4 ksb, u32x4 raw) -> u32x4 {
+        const bool is_ct = i >= 0 && 16 * i < clen;
+        u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
+        uint32_t soff = kOob;
+        if (is_ct) {
+            const int nb = min(16, clen - 16 * i);
+            const u32x4 cur = (ENC && nb < 16) ? shr_bytes(raw, 16 - nb) : raw;
+            out = cur ^ ksb;
+            x = keep_bytes(ENC ? out : cur, nb);
+            uint8_t *ps = scr_wave + (lane_fresh() >> 2) * kScratch;
+            if (nb == 16) soff = cout + 16u * (uint32_t)i;
+            else *(u32x4 *)(ps + kScrTail) = out;
+            if (ENC && i < 2) *(u32x4 *)(ps + 16 * i) = x;
+        } else if (i >= 0 && 16 * i < clen + 16) {
+            x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
+            *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
+        }
+        if (!(QPP_GCM_ABL & 1) || out.x == 0x12345678u)
+            __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
+        return x;
+    };
+    // BPL = 2: lane blocks i and i + 4 (CT indices) in one step
+    auto step2 = [&](int i, bool last, u32x4 raw0, u32x4 raw1, auto first_c) {
+        constexpr bool first = decltype(first_c)::value;
+        const LdsTe Tl{te, (lane_fresh() & 31) * 4};
+        const uint32_t cb0 = (i >= 0 && 16 * i < clen) ? (uint32_t)(i + 2) : 1u;
+        const uint32_t cb1 = (i + 4 >= 0 && 16 * (i + 4) < clen) ? (uint32_t)(i + 6) : 1u;
+        u32x4 ks0, ks1;
+        if constexpr (QPP_GCM_ABL & 8) {
+            ks0 = u32x4{cb0, cc.c0, cc.d0, cc.d1};
+            ks1 = u32x4{cb1, cc.c0, cc.d0, cc.d1};
+        } else if (first && pad >= 4) {
+            // the quad's first four positions are all front padding: only
+            // the second block of the first step is real
+            ks0 = zero4();
+            ks1 = aes_ctr<NR>(cc, cb1, rk, Tl);
+        } else {
+            aes_ctr2<NR>(cc, cb0, cb1, rk, Tl, ks0, ks1);
+        }
+        u32x4 x0 = blk_out(i, ks0, raw0);
+        u32x4 x1 = blk_out(i + 4, ks1, raw1);
+        if constexpr (first) {
+            // position q - 1 = pad holds Z (zero without associated data)
+            if (i == -1) x0 ^= z;
+            if (i + 4 == -1) x1 ^= z;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(QPP_GCM_ABL & 4)) {
+            // (0 ^ 0) H^4 = 0 over front padding
+            if (first && pad >= 4) acc = x1;
+            else acc = ghash_mul_lds(acc ^ x0, G.lds, t4) ^ x1;
+            if (!last) acc = ghash_mul_lds(acc, G.lds, t4);
+        } else {
+            acc ^= x0 ^ x1;
+        }
+    };
 
     got_tag = u32x4{0, 0, 0, 0};
-    if (tiny) {
+    if constexpr (BPL == 2) {
+        if (tiny) {
+            QPP_PROBE_AT(4);
+            const u32x4 st = shl_bytes(*(const u32x4 *)(scr + kScrTail), 16 - rlen);
+            step2(sub - q, true, st, st, std::true_type{});
+        } else {
+            int i = sub - q;
+            // register prefetch of both blocks, one step ahead; on the last
+            // step the first of them is the received tag (unprotect)
+            u32x4 nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i), 0, 0);
+            u32x4 nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i + 4), 0, 0);
+            QPP_PROBE_AT(4);
+            auto one2 = [&](int k, auto first_c) {
+                const u32x4 raw0 = nxt0, raw1 = nxt1;
+                if constexpr (QPP_GCM_ABL & 2) {
+                    nxt0 = u32x4{(uint32_t)k, 0, 0, 0};
+                    nxt1 = nxt0;
+                } else {
+                    const uint32_t l0 = (!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 8);
+                    nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)l0, 0, 0);
+                    nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i + 12), 0, 0);
+                }
+                step2(i, k == 1, raw0, raw1, first_c);
+                i += 8;
+            };
+            // the first step is peeled: it alone may carry Z
+            one2(S, std::true_type{});
+#pragma unroll 1
+            for (int k = S - 1; k > 0; --k) one2(k, std::false_type{});
+            if (!ENC) got_tag = nxt0;
+        }
+    } else if (tiny) {
         // < 16 input bytes: one step (n_a, n_c <= 1), input from LDS
         QPP_PROBE_AT(4);
         // the staged bytes as an end-aligned load would see them
@@ -704,12 +807,12 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
 
 // Output side of a GCM packet after the step loop: partial tail block, tag,
 // header (with header protection for protect), tag check for unprotect.
-template <bool ENC, int SUITE>
+template <bool ENC, int SUITE, int BPL>
 __device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr,
                                            const LdsTe &T, u32x4 tag, u32x4 got_tag)
 {
     const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
-    const int n_g = za + n_c + 1, pad = 4 * ((n_g + 3) >> 2) - n_g;
+    const int n_g = za + n_c + 1, pad = gcm_pad<BPL>(n_g);
     if ((P.clen & 15) && sub == ((pad + za + n_c - 1) & 3))
         st_part(P.dst + P.hlen + 16 * (n_c - 1), *(const u32x4 *)(scr + kScrTail), P.clen & 15);
     // input bytes [0, 16) parked in LDS by the prologue (absent for tiny input)
@@ -1222,7 +1325,7 @@ __device__ __forceinline__ void tab_release(GcmSmem<WG> &sm, uint32_t e)
     if (lane_fresh() == 0) atomicSub(&sm.eref[e], 1u);
 }
 
-template <int SUITE, bool ENC, int WG>
+template <int SUITE, bool ENC, int WG, int BPL>
 __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots,
                                               const uint8_t *__restrict__ gtab, uint32_t cap,
                                               const qpp_desc *__restrict__ desc, uint32_t n,
@@ -1336,7 +1439,7 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
                     QPP_PROBE_AT(3);
                     const GhashTabs G{&sm.h4[0][0], gtab, &sm.wslot[wv], &sm.went[wv]};
                     u32x4 got_tag;
-                    const u32x4 tag = gcm_packet<kNR, ENC>(
+                    const u32x4 tag = gcm_packet<kNR, ENC, BPL>(
                         P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
                         (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0,
 #if QPP_STAGE_LDS
@@ -1354,7 +1457,7 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
                     const LdsTe T2{sm.te, (t2 & 31) * 4};
                     const KeySlot *ks2 =
                         slots + __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
-                    gcm_finish<ENC, SUITE>(P, ks2, t2 & 3, scr2, T2, tag, got_tag);
+                    gcm_finish<ENC, SUITE, BPL>(P, ks2, t2 & 3, scr2, T2, tag, got_tag);
                 } else {
                     P.status = QPP_S_LENGTH;  // the item spans more than 4 GiB
                 }
@@ -1920,6 +2023,18 @@ static int wg_choice(const char *env, int dflt, bool chacha)
     return (w == 512 || w == 768 || w == 1024) ? w : dflt;
 }
 
+// GCM blocks per lane per step (gcm_pad): QPP_GCM_BPL = 1 or 2.  2 (r2i,
+// same box, 2 x 2 runs): north star 1.419 -> 1.389 ms protect (423 -> 435
+// GiB/s), config 4 310 -> 316 GiB/s; WRITE_SIZE 2.08 -> 1.78 GB per 1Mi launch
+static const int kGcmBpl = 2;
+static int gcm_bpl_choice()
+{
+    const char *v = getenv("QPP_GCM_BPL");
+    if (!v) return kGcmBpl;
+    const int b = atoi(v);
+    return (b == 1 || b == 2) ? b : kGcmBpl;
+}
+
 // Persistent GCM grid: one workgroup per CU (the kernel's LDS admits no
 // second), fewer when the batch has fewer than a workgroup's worth of items
 // per CU.
@@ -1957,19 +2072,25 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     const uint32_t *d_items = plan ? plan->d_items : nullptr, *d_irange = plan ? plan->d_irange : nullptr;
     const uint32_t waves = plan ? qpp_internal_plan_max_items(n, kt->cap) : (n + 15) / 16;
     const int wg_gcm = wg_choice("QPP_WG_GCM", kGcmWG, false);
+    const int bpl_gcm = gcm_bpl_choice();
     const int wg_cc = enc ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
                           : wg_choice("QPP_WG_CHACHA_DEC", kChachaWGDec, true);
-#define QPP_LAUNCH_GCM_WG(SUITE, WGV)                                                          \
+#define QPP_LAUNCH_GCM_WGB(SUITE, WGV, BPLV)                                                   \
     do {                                                                                       \
         const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
         if (enc)                                                                               \
-            hipLaunchKernelGGL((k_gcm<SUITE, true, WGV>), grid, block, 0, s, kt->d_slots,      \
+            hipLaunchKernelGGL((k_gcm<SUITE, true, WGV, BPLV>), grid, block, 0, s, kt->d_slots, \
                                kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_items,    \
                                d_irange);                                                      \
         else                                                                                   \
-            hipLaunchKernelGGL((k_gcm<SUITE, false, WGV>), grid, block, 0, s, kt->d_slots,     \
-                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_items,    \
-                               d_irange);                                                      \
+            hipLaunchKernelGGL((k_gcm<SUITE, false, WGV, BPLV>), grid, block, 0, s,            \
+                               kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
+                               d_items, d_irange);                                             \
+    } while (0)
+#define QPP_LAUNCH_GCM_WG(SUITE, WGV)                                                          \
+    do {                                                                                       \
+        if (bpl_gcm == 2) QPP_LAUNCH_GCM_WGB(SUITE, WGV, 2);                                    \
+        else QPP_LAUNCH_GCM_WGB(SUITE, WGV, 1);                                                 \
     } while (0)
 #define QPP_LAUNCH_CHACHA_WG(WGV)                                                              \
     do {                                                                                       \
@@ -1998,6 +2119,7 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     }
 #undef QPP_LAUNCH_GCM
 #undef QPP_LAUNCH_GCM_WG
+#undef QPP_LAUNCH_GCM_WGB
 #undef QPP_LAUNCH_CHACHA_WG
     return QPP_OK;
 }

@@ -141,10 +141,15 @@ def _random_batch(rng, n, n_slots, recs, *, max_payload=1400, pn_lens=(1, 2, 3, 
     return headers, payloads, pns, slots
 
 
+@pytest.mark.parametrize("bpl", ["1", "2"], ids=["gcm-bpl1", "gcm-bpl2"])
 @pytest.mark.parametrize("align", [1, 16])
-def test_random_batch_vs_oracle(oracle, L, engine_cls, align):
-    """Ragged, misaligned packets of all suites and mixed key slots vs the oracle."""
+def test_random_batch_vs_oracle(oracle, L, engine_cls, align, bpl, monkeypatch):
+    """Ragged, misaligned packets of all suites and mixed key slots vs the oracle,
+    under both GCM step forms (QPP_GCM_BPL: one or two blocks per lane a step;
+    the library reads the switch at every launch)."""
     from aioquic_amd.batch import layout_packets
+
+    monkeypatch.setenv("QPP_GCM_BPL", bpl)
 
     rng = np.random.default_rng(0x9001 + align)
     n_slots = 24

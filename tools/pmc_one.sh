@@ -13,7 +13,7 @@ import csv, glob, sys, collections
 d = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_packets" in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in ("k_gcm", "k_chacha", "k_packets")):
             d[(r["Kernel_Name"].split("(")[0][-30:], r["Counter_Name"])].append(float(r["Counter_Value"]))
 for k, v in sorted(d.items()):
     print(k, len(v), sum(v) / len(v))
