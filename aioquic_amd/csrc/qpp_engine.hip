@@ -511,7 +511,7 @@ struct GhashTabs {
     const uint32_t *went;   // LDS: the wave's table entry
     __device__ __forceinline__ uint32_t t4() const
     {
-        return __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)went) * (uint32_t)kGhashPowBytes;
+        return __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)went) * (uint32_t)kGhLdsEntry;
     }
     // the slot's table of H^(pw + 1) in global memory
     __device__ __forceinline__ const uint8_t *global(uint32_t pw) const
@@ -601,14 +601,20 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
         uint32_t soff = kOob;
         if (is_ct) {
-            const int nb = min(16, clen - 16 * i);
-            const u32x4 cur = (ENC && nb < 16) ? shr_bytes(raw, 16 - nb) : raw;
-            out = cur ^ ksb;
-            x = keep_bytes(ENC ? out : cur, nb);
-            uint8_t *ps = scr_wave + (lane_fresh() >> 2) * kScratch;
-            if (nb == 16) soff = cout + 16u * (uint32_t)i;
-            else *(u32x4 *)(ps + kScrTail) = out;
-            if (ENC && i < 2) *(u32x4 *)(ps + 16 * i) = x;
+            const int nb = clen - 16 * i;
+            if (__builtin_expect(nb >= 16, 1)) {
+                // a full block: no byte shifts or masks (a branch, skipped by
+                // the waves whose lanes hold no partial block this step)
+                out = raw ^ ksb;
+                x = ENC ? out : raw;
+                soff = cout + 16u * (uint32_t)i;
+            } else {
+                const u32x4 cur = ENC ? shr_bytes(raw, 16 - nb) : raw;
+                out = cur ^ ksb;
+                x = keep_bytes(ENC ? out : cur, nb);
+                *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrTail) = out;
+            }
+            if (ENC && i < 2) *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + 16 * i) = x;
         } else if (i >= 0 && 16 * i < clen + 16) {
             // lengths block; this lane's AES slot produced E_K(J0) for the tag
             x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
@@ -623,7 +629,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             __builtin_amdgcn_sched_barrier(0);
             // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
             // is applied after the loop
-            if (!last && !(QPP_GCM_ABL & 4)) acc = ghash_mul_lds(acc, G.lds, t4);
+            if (!last && !(QPP_GCM_ABL & 4)) acc = ghash_mul_h4(acc, G.lds, t4);
         }
     };
     // buffer offset of CT block i's input (or out of range)
@@ -638,14 +644,20 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
         uint32_t soff = kOob;
         if (is_ct) {
-            const int nb = min(16, clen - 16 * i);
-            const u32x4 cur = (ENC && nb < 16) ? shr_bytes(raw, 16 - nb) : raw;
-            out = cur ^ ksb;
-            x = keep_bytes(ENC ? out : cur, nb);
-            uint8_t *ps = scr_wave + (lane_fresh() >> 2) * kScratch;
-            if (nb == 16) soff = cout + 16u * (uint32_t)i;
-            else *(u32x4 *)(ps + kScrTail) = out;
-            if (ENC && i < 2) *(u32x4 *)(ps + 16 * i) = x;
+            const int nb = clen - 16 * i;
+            if (__builtin_expect(nb >= 16, 1)) {
+                // a full block: no byte shifts or masks (a branch, skipped by
+                // the waves whose lanes hold no partial block this step)
+                out = raw ^ ksb;
+                x = ENC ? out : raw;
+                soff = cout + 16u * (uint32_t)i;
+            } else {
+                const u32x4 cur = ENC ? shr_bytes(raw, 16 - nb) : raw;
+                out = cur ^ ksb;
+                x = keep_bytes(ENC ? out : cur, nb);
+                *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrTail) = out;
+            }
+            if (ENC && i < 2) *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + 16 * i) = x;
         } else if (i >= 0 && 16 * i < clen + 16) {
             x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
             *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
@@ -683,8 +695,8 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         if constexpr (!(QPP_GCM_ABL & 4)) {
             // (0 ^ 0) H^4 = 0 over front padding
             if (first && pad >= 4) acc = x1;
-            else acc = ghash_mul_lds(acc ^ x0, G.lds, t4) ^ x1;
-            if (!last) acc = ghash_mul_lds(acc, G.lds, t4);
+            else acc = ghash_mul_h4(acc ^ x0, G.lds, t4) ^ x1;
+            if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
         } else {
             acc ^= x0 ^ x1;
         }
@@ -1223,13 +1235,15 @@ __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int su
 // it waits for one to come free.  A share of a bucketed batch walks its
 // slots in order, so the 16 waves hold one or two slots at a time.
 constexpr int kTabEntries = 4;
+static_assert(kGhLdsEntry % 1024 == 0, "LDS-DMA pieces of 1 KiB");
+static_assert(!(QPP_GHASH5 && QPP_FUSE_GH), "the fused GHASH phases read the 4-bit layout");
 
 template <int WG>
 struct __attribute__((aligned(16))) GcmSmem {
     // GHASH table entries first (LDS offset 0: ghash_mul_lds adds e * 8 KiB in
     // its v_perm), then the AES image at 32 KiB; both within the 16-bit
     // ds_read immediate range
-    uint8_t h4[kTabEntries][kGhashPowBytes];  // 32 KiB
+    uint8_t h4[kTabEntries][kGhLdsEntry];     // 56 KiB (QPP_GHASH5) or 32 KiB
     uint8_t te[kTeBytes];                     // Te0|Te1 x 32 bank copies   64 KiB
     uint8_t scratch[WG / 4][kScratch];
 #if QPP_STAGE_LDS
@@ -1300,11 +1314,11 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
     }
     if (e == kNoSlot) return e;  // watchdog: no entry came free (the slot's packets are skipped)
     if (load) {
-        // H^4 (power 3) of the slot: 8 pieces of 1 KiB
-        const uint8_t *src = gtab + (size_t)cur * kGhashTabBytes + 3 * kGhashPowBytes;
+        // H^4 of the slot in the step loop's layout: 13 (or 8) pieces of 1 KiB
+        const uint8_t *src = gtab + (size_t)cur * kGhashTabBytes + (QPP_GHASH5 ? kGh5Off : 3 * kGhashPowBytes);
         const uint32_t l = lane_fresh();
 #pragma unroll
-        for (int c = 0; c < kGhashPowBytes / 1024; ++c)
+        for (int c = 0; c < kGhLdsEntry / 1024; ++c)
             __builtin_amdgcn_global_load_lds((gptr_t)(src + c * 1024 + l * 16), (lptr_t)(sm.h4[e] + c * 1024),
                                              16, 0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1730,6 +1744,24 @@ __global__ __launch_bounds__(kSetupWG) void k_key_setup(KeySlot *__restrict__ sl
             const int byte = w >> 1;
             words[byte >> 2] = (uint32_t)(v << (4 * (w & 1))) << (8 * (byte & 3));
             tab[e] = gf128_mul_slow(u32x4{words[0], words[1], words[2], words[3]}, hpow[p]);
+        }
+        // H^4 in 5-bit windows (ghash_mul_lds5): entry e of window w = the
+        // element with bits [5w, 5w + 5) = e, times H^4; low / high 8 bytes in
+        // 256-byte rows w and kGh5Hi / 256 + w
+        uint32_t *t5 = (uint32_t *)(gtab + (size_t)m.slot * kGhashTabBytes + kGh5Off);
+        for (int i = threadIdx.x; i < kGh5Windows * 32; i += kSetupWG) {
+            const int w = i >> 5, e = i & 31;
+            uint32_t words[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 5; ++b) {
+                const int bit = 5 * w + b;
+                if (bit < 128 && ((e >> b) & 1)) words[bit >> 5] |= 1u << (bit & 31);
+            }
+            const u32x4 v = gf128_mul_slow(u32x4{words[0], words[1], words[2], words[3]}, hpow[3]);
+            uint32_t *row = t5 + w * 64, *rhi = t5 + (kGh5Hi / 4) + w * 64;
+            row[2 * e] = v.x;
+            row[2 * e + 1] = v.y;
+            rhi[2 * e] = v.z;
+            rhi[2 * e + 1] = v.w;
         }
     }
 }
