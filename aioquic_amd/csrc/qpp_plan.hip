@@ -115,6 +115,7 @@ __global__ void k_plan_iranges(const uint32_t *__restrict__ range, const uint32_
 // go back to the caller's order through rsv, so the order is not observable).
 
 constexpr int kScanWG = 1024;
+constexpr int kCntPer = 4;  // packets per thread of k_cnt_keys / k_cnt_scatter
 constexpr uint32_t kMaxBins = 4u << 12;  // 4 buckets x 4096 slots (kPlanCountSlots)
 
 __device__ __forceinline__ uint32_t plan_key(const KeySlot *slots, uint32_t cap, uint32_t s, int slot_bits)
@@ -127,9 +128,11 @@ __device__ __forceinline__ uint32_t plan_key(const KeySlot *slots, uint32_t cap,
     return b << slot_bits | (s < cap ? s : 0u);
 }
 
-// Per-key counts: a workgroup of kScanWG packets counts its keys in an LDS
-// histogram, then adds each non-zero bin to the global one (a batch on one
-// connection would otherwise serialize its atomics on one address).
+// Per-key counts: a workgroup of kCntPer x kScanWG packets counts its keys in
+// an LDS histogram, then adds each non-zero bin to the global one (a batch on
+// one connection would otherwise serialize its atomics on one address).  The
+// histogram's clearing and flushing cost the same for any number of packets,
+// so a workgroup takes several per thread.
 __global__ __launch_bounds__(kScanWG) void k_cnt_keys(const KeySlot *__restrict__ slots, uint32_t cap,
                                                       const qpp_desc *__restrict__ desc, uint32_t n,
                                                       int slot_bits, uint32_t nb, uint32_t *__restrict__ keys,
@@ -138,11 +141,14 @@ __global__ __launch_bounds__(kScanWG) void k_cnt_keys(const KeySlot *__restrict_
     __shared__ uint32_t h[kMaxBins];
     for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) h[b] = 0;
     __syncthreads();
-    const uint32_t i = blockIdx.x * kScanWG + threadIdx.x;
-    if (i < n) {
-        const uint32_t k = plan_key(slots, cap, desc[i].slot, slot_bits);
-        keys[i] = k;
-        atomicAdd(&h[k], 1u);
+#pragma unroll
+    for (int u = 0; u < kCntPer; ++u) {
+        const uint32_t i = (blockIdx.x * kCntPer + u) * kScanWG + threadIdx.x;
+        if (i < n) {
+            const uint32_t k = plan_key(slots, cap, desc[i].slot, slot_bits);
+            keys[i] = k;
+            atomicAdd(&h[k], 1u);
+        }
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += kScanWG)
@@ -152,20 +158,26 @@ __global__ __launch_bounds__(kScanWG) void k_cnt_keys(const KeySlot *__restrict_
 // One workgroup: bins[nb] counts -> posoff / itmoff (exclusive scans of the
 // counts and of their wave items), bins[] = posoff (the scatter cursors),
 // range / irange per bucket, count[24] = wave items in all, items[total] = n.
+// Each thread scans a contiguous run of bins; the LDS copies are padded by one
+// word per 32 (index b + b / 32) so that the threads' runs of 16 hit distinct
+// banks, and every global read and write is coalesced through them.
+__device__ __forceinline__ uint32_t scan_pad(uint32_t b) { return b + (b >> 5); }
+
 __global__ __launch_bounds__(kScanWG) void k_cnt_scan(uint32_t *__restrict__ bins, uint32_t nb, int slot_bits,
                                                       uint32_t n, uint32_t *__restrict__ posoff,
                                                       uint32_t *__restrict__ itmoff,
                                                       uint32_t *__restrict__ count, uint32_t *__restrict__ items)
 {
-    __shared__ uint32_t c[kMaxBins];
+    __shared__ uint32_t c[kMaxBins + kMaxBins / 32], it[kMaxBins + kMaxBins / 32];
     __shared__ uint32_t sp[kScanWG], si[kScanWG];
-    for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) c[b] = bins[b];
+    for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) c[scan_pad(b)] = bins[b];
     __syncthreads();
     const uint32_t per = (nb + kScanWG - 1) / kScanWG, b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
     uint32_t tp = 0, ti = 0;
     for (uint32_t b = b0; b < b1; ++b) {
-        tp += c[b];
-        ti += (c[b] + kItemPackets - 1) / kItemPackets;
+        const uint32_t v = c[scan_pad(b)];
+        tp += v;
+        ti += (v + kItemPackets - 1) / kItemPackets;
     }
     sp[threadIdx.x] = tp;
     si[threadIdx.x] = ti;
@@ -193,17 +205,24 @@ __global__ __launch_bounds__(kScanWG) void k_cnt_scan(uint32_t *__restrict__ bin
                 count[16 + 2 * s - 1] = itm;
             }
         }
-        posoff[b] = pos;
-        itmoff[b] = itm;
-        bins[b] = pos;
-        pos += c[b];
-        itm += (c[b] + kItemPackets - 1) / kItemPackets;
+        const uint32_t v = c[scan_pad(b)];
+        c[scan_pad(b)] = pos;
+        it[scan_pad(b)] = itm;
+        pos += v;
+        itm += (v + kItemPackets - 1) / kItemPackets;
     }
     if (threadIdx.x == 0) {
         count[8 + 7] = n;
         count[16 + 7] = total;
         count[24] = total;
         items[total] = n;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) {
+        const uint32_t v = c[scan_pad(b)];
+        posoff[b] = v;
+        bins[b] = v;
+        itmoff[b] = it[scan_pad(b)];
     }
 }
 
@@ -236,9 +255,13 @@ __global__ __launch_bounds__(kScanWG) void k_cnt_scatter(const uint32_t *__restr
     __shared__ uint32_t h[kMaxBins];
     for (uint32_t b = threadIdx.x; b < nb; b += kScanWG) h[b] = 0;
     __syncthreads();
-    const uint32_t i = blockIdx.x * kScanWG + threadIdx.x;
-    const uint32_t k = i < n ? keys[i] : 0u;
-    const uint32_t r = i < n ? atomicAdd(&h[k], 1u) : 0u;
+    uint32_t k[kCntPer], r[kCntPer];
+#pragma unroll
+    for (int u = 0; u < kCntPer; ++u) {
+        const uint32_t i = (blockIdx.x * kCntPer + u) * kScanWG + threadIdx.x;
+        k[u] = i < n ? keys[i] : 0u;
+        r[u] = i < n ? atomicAdd(&h[k[u]], 1u) : 0u;
+    }
     __syncthreads();
     uint32_t base[kPer];
 #pragma unroll
@@ -254,7 +277,11 @@ __global__ __launch_bounds__(kScanWG) void k_cnt_scatter(const uint32_t *__restr
         if (b < nb) h[b] = base[u];
     }
     __syncthreads();
-    if (i < n) idx[h[k] + r] = i;
+#pragma unroll
+    for (int u = 0; u < kCntPer; ++u) {
+        const uint32_t i = (blockIdx.x * kCntPer + u) * kScanWG + threadIdx.x;
+        if (i < n) idx[h[k[u]] + r[u]] = i;
+    }
 }
 
 // sorted[p] = desc[idx[p]], with the caller's index in rsv
@@ -360,7 +387,7 @@ int qpp_internal_plan_build(qpp_plan *p, const KeySlot *d_slots, uint32_t cap, c
     if (n && cap <= kPlanCountSlots && getenv("QPP_PLAN_RADIX") == nullptr) {
         const uint32_t nb = 4u << sb;
         if (hipMemsetAsync(p->d_bins, 0, nb * 4, s) != hipSuccess) return QPP_E_HIP;
-        const dim3 cgrid((n + kScanWG - 1) / kScanWG);
+        const dim3 cgrid((n + kCntPer * kScanWG - 1) / (kCntPer * kScanWG));
         hipLaunchKernelGGL(k_cnt_keys, cgrid, dim3(kScanWG), 0, s, d_slots, cap, d_desc, n, sb, nb, p->d_keys[0],
                            p->d_bins);
         hipLaunchKernelGGL(k_cnt_scan, dim3(1), dim3(kScanWG), 0, s, p->d_bins, nb, sb, n, p->d_posoff,
