@@ -320,7 +320,23 @@ struct LdsTe {
     {
         return *(const uint32_t *)(te + 128 + addr<3>(s)) & 0xff000000u;
     }
+    // the same entries unmasked: S(x) is byte 1 of fr0 / fr1, byte 2 of fr2,
+    // byte 3 of fr3 (fin_col merges them with two v_perm)
+    __device__ __forceinline__ uint32_t fr0(uint32_t s) const { return *(const uint32_t *)(te + addr<0>(s)); }
+    __device__ __forceinline__ uint32_t fr1(uint32_t s) const { return *(const uint32_t *)(te + addr<1>(s)); }
+    __device__ __forceinline__ uint32_t fr2(uint32_t s) const { return *(const uint32_t *)(te + 128 + addr<2>(s)); }
+    __device__ __forceinline__ uint32_t fr3(uint32_t s) const { return *(const uint32_t *)(te + 128 + addr<3>(s)); }
 };
+
+// One output column of the final round from the raw lookups of LdsTe::fr0..3:
+// bytes S(a0) S(a1) by one v_perm, S(a2) S(a3) by another, then (| , ^ k) in
+// one v_bitop3 -- 3 VALU instead of 4 masks / shifts, 3 ors and an xor.
+__device__ __forceinline__ uint32_t fin_col(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t k)
+{
+    const uint32_t lo = __builtin_amdgcn_perm(r1, r0, 0x0c0c0501u);  // [r0.b1, r1.b1, 0, 0]
+    const uint32_t hi = __builtin_amdgcn_perm(r3, r2, 0x07020c0cu);  // [0, 0, r2.b2, r3.b3]
+    return __builtin_amdgcn_bitop3_b32(lo, hi, k, 0x56);            // (lo | hi) ^ k
+}
 
 // Constant-memory lookups (key setup and other cold paths).
 struct ConstTe {
@@ -387,13 +403,13 @@ __device__ __forceinline__ u32x4 aes_rounds(u32x4 st, const uint32_t *rk, const 
     }
     const uint32_t *k = rk + 4 * NR;
     if constexpr (KROT && kAesGroup) {
-        const uint32_t a0 = T.f0(s0), a1 = T.f1(s1), a2 = T.f2(s2), a3 = T.f3(s3);
-        const uint32_t b0 = T.f0(s1), b1 = T.f1(s2), b2 = T.f2(s3), b3 = T.f3(s0);
-        const uint32_t c0 = T.f0(s2), c1 = T.f1(s3), c2 = T.f2(s0), c3 = T.f3(s1);
-        const uint32_t d0 = T.f0(s3), d1 = T.f1(s0), d2 = T.f2(s1), d3 = T.f3(s2);
+        const uint32_t a0 = T.fr0(s0), a1 = T.fr1(s1), a2 = T.fr2(s2), a3 = T.fr3(s3);
+        const uint32_t b0 = T.fr0(s1), b1 = T.fr1(s2), b2 = T.fr2(s3), b3 = T.fr3(s0);
+        const uint32_t c0 = T.fr0(s2), c1 = T.fr1(s3), c2 = T.fr2(s0), c3 = T.fr3(s1);
+        const uint32_t d0 = T.fr0(s3), d1 = T.fr1(s0), d2 = T.fr2(s1), d3 = T.fr3(s2);
         __builtin_amdgcn_sched_barrier(0);
-        return u32x4{(a0 | a1 | a2 | a3) ^ k[0], (b0 | b1 | b2 | b3) ^ k[1], (c0 | c1 | c2 | c3) ^ k[2],
-                     (d0 | d1 | d2 | d3) ^ k[3]};
+        return u32x4{fin_col(a0, a1, a2, a3, k[0]), fin_col(b0, b1, b2, b3, k[1]), fin_col(c0, c1, c2, c3, k[2]),
+                     fin_col(d0, d1, d2, d3, k[3])};
     }
     return u32x4{(T.f0(s0) | T.f1(s1) | T.f2(s2) | T.f3(s3)) ^ k[0],
                  (T.f0(s1) | T.f1(s2) | T.f2(s3) | T.f3(s0)) ^ k[1],
@@ -488,10 +504,10 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32
     for (int b = 0; b < 2; ++b) {
 #pragma unroll
         for (int col = 0; col < 4; ++col) {
-            f[b][4 * col + 0] = T.f0(s[b][col]);
-            f[b][4 * col + 1] = T.f1(s[b][(col + 1) & 3]);
-            f[b][4 * col + 2] = T.f2(s[b][(col + 2) & 3]);
-            f[b][4 * col + 3] = T.f3(s[b][(col + 3) & 3]);
+            f[b][4 * col + 0] = T.fr0(s[b][col]);
+            f[b][4 * col + 1] = T.fr1(s[b][(col + 1) & 3]);
+            f[b][4 * col + 2] = T.fr2(s[b][(col + 2) & 3]);
+            f[b][4 * col + 3] = T.fr3(s[b][(col + 3) & 3]);
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -500,7 +516,7 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32
     for (int b = 0; b < 2; ++b) {
 #pragma unroll
         for (int col = 0; col < 4; ++col)
-            o[b][col] = (f[b][4 * col] | f[b][4 * col + 1] | f[b][4 * col + 2] | f[b][4 * col + 3]) ^ k[col];
+            o[b][col] = fin_col(f[b][4 * col], f[b][4 * col + 1], f[b][4 * col + 2], f[b][4 * col + 3], k[col]);
     }
     o0 = u32x4{o[0][0], o[0][1], o[0][2], o[0][3]};
     o1 = u32x4{o[1][0], o[1][1], o[1][2], o[1][3]};
@@ -703,11 +719,13 @@ __device__ __forceinline__ void ghash5_group(const uint32_t (&xw)[4], const uint
 #pragma unroll
     for (int i = 0; i < n; ++i) {
         const int w = W0 + i, sb = 5 * w, d = sb >> 5, off = sb & 31;
+        // e = the window's 5 bits: one v_bfe (the compiler's own choice,
+        // shift + mask + or with tsel, is one VALU more per window)
         uint32_t e;
-        if (off <= 27) e = (xw[d] >> off) & 31u;
+        if (off <= 27) asm("v_bfe_u32 %0, %1, %2, 5" : "=v"(e) : "v"(xw[d]), "i"(off));
         else if (d < 3) e = __builtin_amdgcn_alignbit(xw[d + 1], xw[d], off) & 31u;
         else e = xw[3] >> off;  // bits past 127 are zero
-        const uint32_t a = (e << 3) + tsel;
+        const uint32_t a = (e << 3) | tsel;  // tsel: a multiple of 1 KiB
         lo[i] = *(const u32x2 *)(base + w * 256 + a);
         hi[i] = *(const u32x2 *)(base + kGh5Hi + w * 256 + a);
     }
