@@ -2476,6 +2476,10 @@ static int session_drain_on_error(qpp_session *s, int rc)
     return rc;
 }
 
+constexpr uint32_t kSmallPackets = 64;
+constexpr size_t kSmallBytes = (size_t)256 << 10;
+static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp_desc *desc,
                        uint32_t n, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len,
                        qpp_result *res)
@@ -2495,6 +2499,31 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
         if (mono)
             return session_run_pipelined(enc, s, kt, desc, n, in, in_len, out, out_len, res,
                                          chunks);
+    }
+    // Small batches (the per-call object API: one packet per call): one H2D
+    // copy of [descriptors | input | zeroed output] and one D2H copy of
+    // [output | results] through the session's input staging, instead of
+    // four copies and a device memset.
+    const size_t sd = al256((size_t)n * sizeof(qpp_desc)), si = al256(in_len), so = al256(out_len);
+    const size_t small = sd + si + so + (size_t)n * sizeof(qpp_result);
+    if (n <= kSmallPackets && small <= kSmallBytes && in != s->h_in && out != s->h_out) {
+        rc = session_reserve(s, small > need ? small : need, n);
+        if (rc != QPP_OK) return rc;
+        uint8_t *h = s->h_in, *d = s->d_in;
+        memcpy(h, desc, (size_t)n * sizeof(qpp_desc));
+        reject_out_of_bounds(enc, (qpp_desc *)h, n, in_len, out_len);
+        if (in_len) memcpy(h + sd, in, in_len);
+        memset(h + sd + si, 0, out_len);  // bytes the kernel does not write come back as zeros
+        HIPCHK(hipMemcpyAsync(d, h, sd + si + out_len, hipMemcpyHostToDevice, s->stream));
+        rc = launch_packets(enc, kt, (const qpp_desc *)d, n, d + sd, d + sd + si,
+                            (qpp_result *)(d + sd + si + so), s->stream);
+        if (rc != QPP_OK) return rc;
+        HIPCHK(hipMemcpyAsync(h + sd + si, d + sd + si, so + (size_t)n * sizeof(qpp_result),
+                              hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (out_len) memcpy(out, h + sd + si, out_len);
+        memcpy(res, h + sd + si + so, (size_t)n * sizeof(qpp_result));
+        return QPP_OK;
     }
     qpp_desc *hd = (qpp_desc *)s->h_misc;
     qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
