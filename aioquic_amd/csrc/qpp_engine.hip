@@ -920,7 +920,10 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
     const uint32_t qoff = (lane_fresh() >> 2) * 64;  // the quad's 64 bytes in each region
 
     dma(0);
-    P130 acc = p130_zero(), r = p130_zero(), r12 = p130_zero();
+    // r13 = r^13: the multiply of a lane's last block before its next chunk
+    // also jumps over the other 3 lanes' chunks (12 blocks), so a chunk costs
+    // 4 multiplies instead of 4 + 1
+    P130 acc = p130_zero(), r = p130_zero(), r13 = p130_zero();
     int g_last = -1;
 #pragma unroll 1
     for (int k = 0; k < steps; ++k) {
@@ -935,8 +938,9 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
             *(u32x4 *)(scr + 64) = u32x4{kw[4], kw[5], kw[6], kw[7]};
             r = p130_r(kw[0], kw[1], kw[2], kw[3]);
             const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2);
-            r12 = p130_mul(p130_mul(r4, r4), r4);
-            // lane 0 starts its chain with the associated data
+            r13 = p130_mul(p130_mul(p130_mul(r4, r4), r4), r);
+            // lane 0 starts its chain with the associated data (its next
+            // chunk, if any, is chunk 3)
             if (sub == 0) {
                 for (int g = 0; g < n_a; ++g) {
                     const int nb = min(16, P.hlen - 16 * g);
@@ -944,7 +948,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
                                              : ld_win(P.src + 16 * g, nb, P.src, P.src + rlen);
                     if (unmask) a ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
                     if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
-                    acc = p130_mul(p130_add(acc, p130_block(a)), r);
+                    acc = p130_mul(p130_add(acc, p130_block(a)), (g == n_a - 1 && 3 < chunks) ? r13 : r);
                     g_last = g;
                 }
             }
@@ -988,11 +992,11 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         __builtin_amdgcn_wave_barrier();
         if (k + 1 < steps) dma(k + 1);
         if (c >= 0 && c < chunks) {
-            if (g_last >= 0) acc = p130_mul(acc, r12);  // the 3 other lanes' chunks (12 blocks)
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 if (4 * c + b >= n_c) break;
-                acc = p130_mul(p130_add(acc, p130_block(x[b])), r);
+                // block 3 of a chunk the lane follows with chunk c + 4: r^13
+                acc = p130_mul(p130_add(acc, p130_block(x[b])), (b == 3 && c + 4 < chunks) ? r13 : r);
                 g_last = n_a + 4 * c + b;
             }
         }
