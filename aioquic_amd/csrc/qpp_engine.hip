@@ -918,6 +918,10 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         for (int t = 0; t < 4; ++t) lds_dma16(B.in, stage + t * kChRegion, blk_off(4 * (4 * k - 1 + t) + sub));
     };
     const uint32_t qoff = (lane_fresh() >> 2) * 64;  // the quad's 64 bytes in each region
+    // the packet fields the chunk loop does not use (HP mask, packet number,
+    // header layout) wait in LDS until the tag: 128 VGPRs at 4 waves per SIMD
+    // leave no room for them across the loop
+    park(P, scr);
 
     dma(0);
     // r13 = r^13: the multiply of a lane's last block before its next chunk
@@ -935,18 +939,19 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
             uint32_t kw[8];
 #pragma unroll
             for (int w = 0; w < 8; ++w) kw[w] = quad_dpp<0x00>(blk[w]);
-            *(u32x4 *)(scr + 64) = u32x4{kw[4], kw[5], kw[6], kw[7]};
+            *(u32x4 *)(scr + kScrEj0) = u32x4{kw[4], kw[5], kw[6], kw[7]};
             r = p130_r(kw[0], kw[1], kw[2], kw[3]);
             const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2);
             r13 = p130_mul(p130_mul(p130_mul(r4, r4), r4), r);
             // lane 0 starts its chain with the associated data (its next
             // chunk, if any, is chunk 3)
             if (sub == 0) {
+                const Pkt Q = unpark(scr, P.src, P.dst);
                 for (int g = 0; g < n_a; ++g) {
                     const int nb = min(16, P.hlen - 16 * g);
                     u32x4 a = (g == 0 && h0) ? keep_bytes(*(const u32x4 *)h0, nb)
                                              : ld_win(P.src + 16 * g, nb, P.src, P.src + rlen);
-                    if (unmask) a ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
+                    if (unmask) a ^= hp_pattern(16 * g, Q.mask, Q.fbm, Q.pn_off, Q.pn_len);
                     if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
                     acc = p130_mul(p130_add(acc, p130_block(a)), (g == n_a - 1 && 3 < chunks) ? r13 : r);
                     g_last = g;
@@ -1001,6 +1006,11 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
             }
         }
     }
+    {
+        const uint8_t *src = P.src;
+        uint8_t *dst = P.dst;
+        P = unpark(scr, src, dst);
+    }
     // acc = sum m_g r^(g_last - g + 1); scale to r^(n_g - g) with r^(n_g - 1 - g_last)
     int e = n_g - 1 - g_last;
     if (g_last < 0) e = 0;
@@ -1025,7 +1035,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
     }
     const u32x4 lens = u32x4{(uint32_t)P.hlen, 0u, (uint32_t)P.clen, 0u};
     sum = p130_mul(p130_add(sum, p130_block(lens)), r);
-    const u32x4 sw = *(const u32x4 *)(scr + 64);
+    const u32x4 sw = *(const u32x4 *)(scr + kScrEj0);
     const u32x4 tag = p130_finish(sum, sw.x, sw.y, sw.z, sw.w);
     if (ENC) {
         if (sub == 0) st16(pout + P.clen, tag);
