@@ -706,54 +706,113 @@ __device__ __forceinline__ u32x4 ghash_mul_lds(u32x4 x, const uint8_t *base, uin
     return acc;
 }
 
-// x * H^4 from a 5-bit-window table (kGh5Bytes) at LDS `base` + tsel.  Four
-// groups of <= 7 windows, each group's 14 ds_read_b64 in flight before the
-// first use (28 VGPRs).  A window's entry offset e * 8 + tsel is one v_bfe
-// and one v_lshl_add; the window's row offset rides in the ds_read immediate.
+// x * H^4 from a 5-bit-window table (kGh5Bytes) at LDS `base` + tsel, in
+// groups of windows.  A window's entry offset e * 8 + tsel is one v_bfe and
+// one v_lshl_or; the window's row offset rides in the ds_read immediate.
+// One group of windows [W0, W1): its reads (issue) and their sum (consume).
 template <int W0, int W1>
-__device__ __forceinline__ void ghash5_group(const uint32_t (&xw)[4], const uint8_t *base, uint32_t tsel,
-                                             u32x4 &acc)
-{
-    constexpr int n = W1 - W0;
-    u32x2 lo[n], hi[n];
+struct Gh5Grp {
+    u32x2 lo[W1 - W0], hi[W1 - W0];
+    __device__ __forceinline__ void issue(const uint32_t (&xw)[4], const uint8_t *base, uint32_t tsel)
+    {
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
-        const int w = W0 + i, sb = 5 * w, d = sb >> 5, off = sb & 31;
-        // e = the window's 5 bits: one v_bfe (the compiler's own choice,
-        // shift + mask + or with tsel, is one VALU more per window)
-        uint32_t e;
-        if (off <= 27) asm("v_bfe_u32 %0, %1, %2, 5" : "=v"(e) : "v"(xw[d]), "i"(off));
-        else if (d < 3) e = __builtin_amdgcn_alignbit(xw[d + 1], xw[d], off) & 31u;
-        else e = xw[3] >> off;  // bits past 127 are zero
-        const uint32_t a = (e << 3) | tsel;  // tsel: a multiple of 1 KiB
-        lo[i] = *(const u32x2 *)(base + w * 256 + a);
-        hi[i] = *(const u32x2 *)(base + kGh5Hi + w * 256 + a);
+        for (int i = 0; i < W1 - W0; ++i) {
+            const int w = W0 + i, sb = 5 * w, d = sb >> 5, off = sb & 31;
+            // e = the window's 5 bits: one v_bfe (the compiler's own choice,
+            // shift + mask + or with tsel, is one VALU more per window)
+            uint32_t e;
+            if (off <= 27) asm("v_bfe_u32 %0, %1, %2, 5" : "=v"(e) : "v"(xw[d]), "i"(off));
+            else if (d < 3) e = __builtin_amdgcn_alignbit(xw[d + 1], xw[d], off) & 31u;
+            else e = xw[3] >> off;  // bits past 127 are zero
+            const uint32_t a = (e << 3) | tsel;  // tsel: a multiple of 1 KiB
+            lo[i] = *(const u32x2 *)(base + w * 256 + a);
+            hi[i] = *(const u32x2 *)(base + kGh5Hi + w * 256 + a);
+        }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    __device__ __forceinline__ void consume(u32x4 &acc) const
+    {
+        constexpr int n = W1 - W0;
 #pragma unroll
-    for (int i = 0; i + 1 < n; i += 2) {
-        acc.x = xor3(acc.x, lo[i].x, lo[i + 1].x);
-        acc.y = xor3(acc.y, lo[i].y, lo[i + 1].y);
-        acc.z = xor3(acc.z, hi[i].x, hi[i + 1].x);
-        acc.w = xor3(acc.w, hi[i].y, hi[i + 1].y);
+        for (int i = 0; i + 1 < n; i += 2) {
+            acc.x = xor3(acc.x, lo[i].x, lo[i + 1].x);
+            acc.y = xor3(acc.y, lo[i].y, lo[i + 1].y);
+            acc.z = xor3(acc.z, hi[i].x, hi[i + 1].x);
+            acc.w = xor3(acc.w, hi[i].y, hi[i + 1].y);
+        }
+        if constexpr (n & 1) {
+            acc.x ^= lo[n - 1].x;
+            acc.y ^= lo[n - 1].y;
+            acc.z ^= hi[n - 1].x;
+            acc.w ^= hi[n - 1].y;
+        }
     }
-    if constexpr (n & 1) {
-        acc.x ^= lo[n - 1].x;
-        acc.y ^= lo[n - 1].y;
-        acc.z ^= hi[n - 1].x;
-        acc.w ^= hi[n - 1].y;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-}
+};
 
+#ifndef QPP_GHASH5_PIPE
+#define QPP_GHASH5_PIPE 1
+#endif
+// Six groups software-pipelined (QPP_GHASH5_PIPE): group g + 1's reads are
+// in flight while group g is summed, so a multiply pays about one LDS round
+// trip instead of one per group; at most two groups' reads (<= 40 VGPRs)
+// are held.  0: four groups, each drained before the next is issued.
 __device__ __forceinline__ u32x4 ghash_mul_lds5(u32x4 x, const uint8_t *base, uint32_t tsel)
 {
     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
     u32x4 acc = {0, 0, 0, 0};
-    ghash5_group<0, 7>(xw, base, tsel, acc);
-    ghash5_group<7, 13>(xw, base, tsel, acc);
-    ghash5_group<13, 20>(xw, base, tsel, acc);
-    ghash5_group<20, kGh5Windows>(xw, base, tsel, acc);
+#define QPP_SB() __builtin_amdgcn_sched_barrier(0)
+    if constexpr (QPP_GHASH5_PIPE) {
+        Gh5Grp<0, 5> a;
+        Gh5Grp<5, 9> b;
+        Gh5Grp<9, 14> c;
+        Gh5Grp<14, 18> d;
+        Gh5Grp<18, 22> e;
+        Gh5Grp<22, kGh5Windows> f;
+        a.issue(xw, base, tsel);
+        b.issue(xw, base, tsel);
+        QPP_SB();
+        a.consume(acc);
+        QPP_SB();
+        c.issue(xw, base, tsel);
+        QPP_SB();
+        b.consume(acc);
+        QPP_SB();
+        d.issue(xw, base, tsel);
+        QPP_SB();
+        c.consume(acc);
+        QPP_SB();
+        e.issue(xw, base, tsel);
+        QPP_SB();
+        d.consume(acc);
+        QPP_SB();
+        f.issue(xw, base, tsel);
+        QPP_SB();
+        e.consume(acc);
+        QPP_SB();
+        f.consume(acc);
+        QPP_SB();
+    } else {
+        Gh5Grp<0, 7> a;
+        Gh5Grp<7, 13> b;
+        Gh5Grp<13, 20> c;
+        Gh5Grp<20, kGh5Windows> d;
+        a.issue(xw, base, tsel);
+        QPP_SB();
+        a.consume(acc);
+        QPP_SB();
+        b.issue(xw, base, tsel);
+        QPP_SB();
+        b.consume(acc);
+        QPP_SB();
+        c.issue(xw, base, tsel);
+        QPP_SB();
+        c.consume(acc);
+        QPP_SB();
+        d.issue(xw, base, tsel);
+        QPP_SB();
+        d.consume(acc);
+        QPP_SB();
+    }
+#undef QPP_SB
     return acc;
 }
 
