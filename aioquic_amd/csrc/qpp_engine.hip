@@ -60,7 +60,7 @@ constexpr bool kFuseGh = QPP_FUSE_GH;
 #define QPP_CHACHA_WPE 4  // ChaCha20-Poly1305: minimum waves per SIMD (4: 128 VGPRs, 8 spilled; r2i same box vs 1 (146 VGPRs, 3 waves): 64Ki +4 %, 1Mi +1 %, config 5 +1 %)
 #endif
 #ifndef QPP_GCM_PF
-#define QPP_GCM_PF 1  // GCM step input: register prefetch distance in steps (1, or 2: same time on 1Mi and config 4, +6 VGPRs)
+#define QPP_GCM_PF 1  // GCM step input: register prefetch distance in steps (2: BPL 1 same time, BPL 2 -0.6 % with 2-4 VGPRs spilled; r2k)
 #endif
 #ifndef QPP_GCM_ABL
 #define QPP_GCM_ABL 0  // ablation study only (wrong output): step loop without 1 stores, 2 loads, 4 GHASH, 8 AES
@@ -714,6 +714,27 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             // step the first of them is the received tag (unprotect)
             u32x4 nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i), 0, 0);
             u32x4 nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i + 4), 0, 0);
+#if QPP_GCM_PF >= 2
+            // two steps ahead (A/B switch): the loads of the step with `rem`
+            // steps left, starting at CT block j (rem 0: the received tag)
+            auto load_for = [&](int rem, int j, u32x4 &a, u32x4 &b) {
+                const uint32_t l0 = rem >= 1 ? ct_load(j) : (rem == 0 && !ENC) ? cin + (uint32_t)clen : kOob;
+                const uint32_t l1 = rem >= 1 ? ct_load(j + 4) : kOob;
+                a = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)l0, 0, 0);
+                b = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)l1, 0, 0);
+            };
+            u32x4 nxt2, nxt3;
+            load_for(S - 1, i + 8, nxt2, nxt3);
+            QPP_PROBE_AT(4);
+            auto one2 = [&](int k, auto first_c) {
+                const u32x4 raw0 = nxt0, raw1 = nxt1;
+                nxt0 = nxt2;
+                nxt1 = nxt3;
+                load_for(k - 2, i + 16, nxt2, nxt3);
+                step2(i, k == 1, raw0, raw1, first_c);
+                i += 8;
+            };
+#else
             QPP_PROBE_AT(4);
             auto one2 = [&](int k, auto first_c) {
                 const u32x4 raw0 = nxt0, raw1 = nxt1;
@@ -728,6 +749,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                 step2(i, k == 1, raw0, raw1, first_c);
                 i += 8;
             };
+#endif
             // the first step is peeled: it alone may carry Z
             one2(S, std::true_type{});
 #pragma unroll 1
