@@ -989,17 +989,26 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         for (int b = 0; b < 4; ++b) {
             const int i = 4 * c + b;
             const bool valid = c >= 0 && i < n_c;
-            const int nb = min(16, P.clen - 16 * i);
+            const int nb = P.clen - 16 * i;
             u32x4 in = *(const u32x4 *)(mine + 16 * b);
-            if (tiny) in = valid ? ld_part(pin + 16 * i, nb) : in;
-            else if (ENC && nb < 16) in = shr_bytes(in, 16 - nb);
-            const u32x4 o = in ^ u32x4{blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3]};
+            const u32x4 ks = u32x4{blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3]};
+            u32x4 o;
             x[b] = u32x4{0, 0, 0, 0};
-            if (valid) {
-                x[b] = keep_bytes(ENC ? o : in, nb);
-                if (nb < 16) st_part(pout + 16 * i, o, nb);  // partial block: byte-exact, direct
-                if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[b];
+            if (__builtin_expect(valid && nb >= 16 && !tiny, 1)) {
+                // a full block: no byte shifts or masks (a branch, skipped by
+                // the waves whose lanes hold no partial block this step)
+                o = in ^ ks;
+                x[b] = ENC ? o : in;
+            } else {
+                if (tiny) in = valid ? ld_part(pin + 16 * i, min(16, nb)) : in;
+                else if (ENC && nb < 16) in = shr_bytes(in, 16 - nb);
+                o = in ^ ks;
+                if (valid) {
+                    x[b] = keep_bytes(ENC ? o : in, min(16, nb));
+                    if (nb < 16) st_part(pout + 16 * i, o, nb);  // partial block: byte-exact, direct
+                }
             }
+            if (valid && ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[b];
             *(u32x4 *)(mine + 16 * b) = o;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
