@@ -19,6 +19,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 
 from . import layout as L
@@ -110,8 +112,11 @@ def make_workload(n: int, suite=L.AES_128_GCM, n_keys: int = 1, seed: int = 0x90
         elif order != "round_robin":
             raise ValueError(f"unknown order {order!r}")
 
-    plain = np.zeros(n * SLOT_BYTES, dtype=np.uint8)
-    view = plain.reshape(n, SLOT_BYTES)
+    # layout study only (QPP_BENCH_SHIFT=k): the whole batch starts k bytes
+    # into its buffers, e.g. 5 puts every payload on a 16-byte boundary
+    shift = int(os.environ.get("QPP_BENCH_SHIFT", "0"))
+    plain = np.zeros(n * SLOT_BYTES + shift, dtype=np.uint8)
+    view = plain[shift:].reshape(n, SLOT_BYTES)
     view[:, 0] = 0x41
     view[:, 1:9] = np.frombuffer(DCID, np.uint8)
     view[:, 9] = ((pn >> 8) & 0xFF).astype(np.uint8)
@@ -128,6 +133,7 @@ def make_workload(n: int, suite=L.AES_128_GCM, n_keys: int = 1, seed: int = 0x90
         offs = np.arange(n, dtype=np.uint64) * SLOT_BYTES
     else:
         raise ValueError(f"unknown layout {layout!r}")
+    offs = offs + np.uint64(shift)
     desc = np.zeros(n, dtype=L.DESC)
     desc["in_off"] = offs
     desc["out_off"] = offs
@@ -139,5 +145,5 @@ def make_workload(n: int, suite=L.AES_128_GCM, n_keys: int = 1, seed: int = 0x90
     udesc["len"] = SLOT_BYTES
     udesc["hdr_len"] = PN_OFF
     return Workload(n=n, n_keys=n_keys, keys=keys, desc=desc, udesc=udesc, plain=plain,
-                    plain_size=n * SLOT_BYTES, wire_size=n * SLOT_BYTES,
+                    plain_size=n * SLOT_BYTES + shift, wire_size=n * SLOT_BYTES + shift,
                     suites=keys["suite"][key_of])
