@@ -59,6 +59,9 @@ constexpr bool kFuseGh = QPP_FUSE_GH;
 #ifndef QPP_CHACHA_WPE
 #define QPP_CHACHA_WPE 4  // ChaCha20-Poly1305: minimum waves per SIMD (4: 128 VGPRs, 8 spilled; r2i same box vs 1 (146 VGPRs, 3 waves): 64Ki +4 %, 1Mi +1 %, config 5 +1 %)
 #endif
+#ifndef QPP_GCM_PRIO
+#define QPP_GCM_PRIO 0  // study: s_setprio 1 over each step's GHASH phase (1) or AES phase (2)
+#endif
 #ifndef QPP_GCM_PF
 #define QPP_GCM_PF 1  // GCM step input: register prefetch distance in steps (2: BPL 1 same time, BPL 2 -0.6 % with 2-4 VGPRs spilled; r2k)
 #endif
@@ -673,6 +676,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         const uint32_t cb0 = (i >= 0 && 16 * i < clen) ? (uint32_t)(i + 2) : 1u;
         const uint32_t cb1 = (i + 4 >= 0 && 16 * (i + 4) < clen) ? (uint32_t)(i + 6) : 1u;
         u32x4 ks0, ks1;
+        if constexpr (QPP_GCM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         if constexpr (QPP_GCM_ABL & 8) {
             ks0 = u32x4{cb0, cc.c0, cc.d0, cc.d1};
             ks1 = u32x4{cb1, cc.c0, cc.d0, cc.d1};
@@ -684,6 +688,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         } else {
             aes_ctr2<NR>(cc, cb0, cb1, rk, Tl, ks0, ks1);
         }
+        if constexpr (QPP_GCM_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         u32x4 x0 = blk_out(i, ks0, raw0);
         u32x4 x1 = blk_out(i + 4, ks1, raw1);
         if constexpr (first) {
@@ -692,6 +697,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             if (i + 4 == -1) x1 ^= z;
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (QPP_GCM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
         if constexpr (!(QPP_GCM_ABL & 4)) {
             // (0 ^ 0) H^4 = 0 over front padding
             if (first && pad >= 4) acc = x1;
@@ -700,6 +706,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         } else {
             acc ^= x0 ^ x1;
         }
+        if constexpr (QPP_GCM_PRIO != 0) __builtin_amdgcn_s_setprio(0);
     };
 
     got_tag = u32x4{0, 0, 0, 0};
