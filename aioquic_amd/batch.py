@@ -146,9 +146,14 @@ class PacketEngine:
 
 
 def layout_packets(headers, payloads, pns, slots, *, align: int = 1, tag_room: bool = True,
-                   flags: int = 0):
+                   flags: int = 0, payload_align: int = 1):
     """Pack (header, payload) pairs into one input buffer and build protect
     descriptors whose outputs go to the same offsets of an output buffer.
+
+    align: each packet starts on a multiple of it.  payload_align: each
+    packet is placed so that its payload (after the header) starts on a
+    multiple of it instead -- 16 saves the kernels' 16-byte loads and stores
+    a second segment each (Payload alignment).
 
     Returns (inbuf uint8 array, desc array, out_size)."""
     n = len(headers)
@@ -157,7 +162,11 @@ def layout_packets(headers, payloads, pns, slots, *, align: int = 1, tag_room: b
     offs = np.zeros(n, dtype=np.int64)
     pos = 0
     for i, s in enumerate(sizes):
-        pos = (pos + align - 1) // align * align
+        if payload_align > 1:
+            hl = len(headers[i])
+            pos = (pos + hl + payload_align - 1) // payload_align * payload_align - hl
+        else:
+            pos = (pos + align - 1) // align * align
         offs[i] = pos
         pos += s
     buf = np.zeros(pos + 16, dtype=np.uint8)

@@ -142,22 +142,24 @@ def _random_batch(rng, n, n_slots, recs, *, max_payload=1400, pn_lens=(1, 2, 3, 
 
 
 @pytest.mark.parametrize("bpl", ["1", "2"], ids=["gcm-bpl1", "gcm-bpl2"])
-@pytest.mark.parametrize("align", [1, 16])
+@pytest.mark.parametrize("align", [1, 16, -16], ids=["align1", "align16", "payload16"])
 def test_random_batch_vs_oracle(oracle, L, engine_cls, align, bpl, monkeypatch):
     """Ragged, misaligned packets of all suites and mixed key slots vs the oracle,
     under both GCM step forms (QPP_GCM_BPL: one or two blocks per lane a step;
-    the library reads the switch at every launch)."""
+    the library reads the switch at every launch); align < 0: payloads on
+    multiples of -align (layout_packets(payload_align=...))."""
     from aioquic_amd.batch import layout_packets
 
     monkeypatch.setenv("QPP_GCM_BPL", bpl)
 
-    rng = np.random.default_rng(0x9001 + align)
+    rng = np.random.default_rng(0x9001 + abs(align))
     n_slots = 24
     recs = _keys(rng, n_slots)
     eng = engine_cls(n_slots)
     eng.set_key_records(recs)
     headers, payloads, pns, slots = _random_batch(rng, 3000, n_slots, recs)
-    inbuf, desc, size = layout_packets(headers, payloads, pns, slots, align=align)
+    inbuf, desc, size = layout_packets(headers, payloads, pns, slots, align=max(align, 1),
+                                       payload_align=max(-align, 1))
     out_g, res_g = eng.protect_host(desc, inbuf.tobytes(), size)
     out_o, res_o = oracle.protect_batch(recs, desc, inbuf, size)
     assert (res_g["status"] == res_o["status"]).all()
