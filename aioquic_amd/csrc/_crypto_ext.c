@@ -750,7 +750,9 @@ static PyObject *batch_list(PyObject *args, int enc)
         Py_ssize_t l1, l2 = 0;
         if (PyBytes_AsStringAndSize(PyList_GetItem(items, i), &b, &l1) < 0) return NULL;
         if (enc && PyBytes_AsStringAndSize(PyList_GetItem(payloads, i), &b, &l2) < 0) return NULL;
-        total += (size_t)l1 + (size_t)l2 + (enc ? QPP_TAG_LEN : 0);
+        /* protect: up to 15 bytes of room to start each payload on a
+           16-byte boundary (Payload alignment) */
+        total += (size_t)l1 + (size_t)l2 + (enc ? QPP_TAG_LEN + 15 : 0);
     }
     qpp_session *s = session();
     if (!s) return NULL;
@@ -776,6 +778,7 @@ static PyObject *batch_list(PyObject *args, int enc)
             (void)PyBytes_AsStringAndSize(PyList_GetItem(items, i), &b1, &l1);
             if (enc) (void)PyBytes_AsStringAndSize(PyList_GetItem(payloads, i), &b2, &l2);
             qpp_desc *d = &desc[i];
+            if (enc) off = ((off + (size_t)l1 + 15) & ~(size_t)15) - (size_t)l1;
             d->in_off = d->out_off = off;
             uint64_t num;
             memcpy(&num, nums + 8 * i, 8);
