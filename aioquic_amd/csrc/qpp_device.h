@@ -78,7 +78,7 @@ constexpr int kGhashPowers = 4;
 constexpr int kGhashPowBytes = 32 * 16 * 16;  // one power: 32 windows x 16 nibbles x 16 B
 
 // H^4 once more, for the GCM step loop's LDS entries, in 5-bit windows
-// (QPP_GHASH5): window w = bits [5w, 5w + 5) of the block as a little-endian
+// window w = bits [5w, 5w + 5) of the block as a little-endian
 // 128-bit integer (26 windows, the last 3 bits wide) -> 32 entries of 16 B,
 // stored as a low 8-byte half (one 256 B row per window, rows 0-25) and a
 // high half (rows 27-52: 6912 B further, a distance no ds_read2 form can
@@ -88,16 +88,13 @@ constexpr int kGhashPowBytes = 32 * 16 * 16;  // one power: 32 windows x 16 nibb
 // 64 distinct banks whatever their entries (MI355X_MICROARCH.md, LDS): a
 // multiply is 52 reads x 2 LDS cycles = 104 against 32 ds_read_b128 x 4 = 128
 // for the 4-bit windows, and fewer VALU for the window extraction.
-#ifndef QPP_GHASH5
-#define QPP_GHASH5 1
-#endif
 constexpr int kGh5Windows = 26;
 constexpr int kGh5Hi = 27 * 256;  // offset of the high halves
 constexpr int kGh5Bytes = 14 * 1024;
 constexpr int kGh5Off = kGhashPowers * kGhashPowBytes;  // offset of the 5-bit H^4 in a slot's tables
 constexpr int kGhashTabBytes = kGh5Off + kGh5Bytes;      // 46 KiB per slot
 // one LDS table entry of the GCM kernel: H^4 in the step loop's layout
-constexpr int kGhLdsEntry = QPP_GHASH5 ? kGh5Bytes : kGhashPowBytes;
+constexpr int kGhLdsEntry = kGh5Bytes;
 
 // ---------------------------------------------------------------- helpers --
 
@@ -352,13 +349,6 @@ struct ConstTe {
     __device__ __forceinline__ uint32_t f3(uint32_t s) const { return (uint32_t)c_aes.sbox[s >> 24] << 24; }
 };
 
-// Issue grouping of the counter-mode rounds (A/B switch, QPP_AES_GROUP=0 is
-// the compiler's own schedule).
-#ifndef QPP_AES_GROUP
-#define QPP_AES_GROUP 1
-#endif
-constexpr bool kAesGroup = QPP_AES_GROUP;
-
 // One AES encryption, state and round keys as little-endian column words.
 // Round: column c takes row r from column c+r (ShiftRows) through Te_r
 // (MixColumns coefficients); the final round substitutes only.
@@ -375,7 +365,7 @@ __device__ __forceinline__ u32x4 aes_rounds(u32x4 st, const uint32_t *rk, const 
     for (int r = R0; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
         uint32_t t0, t1, t2, t3;
-        if constexpr (KROT && kAesGroup) {
+        if constexpr (KROT) {
             // all 16 lookups of the round in flight before the first use: one
             // LDS round trip per round (the scheduler otherwise interleaves
             // waits after every few reads to save registers)
@@ -388,11 +378,6 @@ __device__ __forceinline__ u32x4 aes_rounds(u32x4 st, const uint32_t *rk, const 
             t1 = xor3(b0, b1, rotl(xor3(b2, b3, k[1]), 16));
             t2 = xor3(c0, c1, rotl(xor3(c2, c3, k[2]), 16));
             t3 = xor3(d0, d1, rotl(xor3(d2, d3, k[3]), 16));
-        } else if constexpr (KROT) {
-            t0 = xor3(T.t0(s0), T.t1(s1), rotl(xor3(T.t2r(s2), T.t3r(s3), k[0]), 16));
-            t1 = xor3(T.t0(s1), T.t1(s2), rotl(xor3(T.t2r(s3), T.t3r(s0), k[1]), 16));
-            t2 = xor3(T.t0(s2), T.t1(s3), rotl(xor3(T.t2r(s0), T.t3r(s1), k[2]), 16));
-            t3 = xor3(T.t0(s3), T.t1(s0), rotl(xor3(T.t2r(s1), T.t3r(s2), k[3]), 16));
         } else {
             t0 = xor3(xor3(T.t0(s0), T.t1(s1), T.t2(s2)), T.t3(s3), k[0]);
             t1 = xor3(xor3(T.t0(s1), T.t1(s2), T.t2(s3)), T.t3(s0), k[1]);
@@ -402,7 +387,7 @@ __device__ __forceinline__ u32x4 aes_rounds(u32x4 st, const uint32_t *rk, const 
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint32_t *k = rk + 4 * NR;
-    if constexpr (KROT && kAesGroup) {
+    if constexpr (KROT) {
         const uint32_t a0 = T.fr0(s0), a1 = T.fr1(s1), a2 = T.fr2(s2), a3 = T.fr3(s3);
         const uint32_t b0 = T.fr0(s1), b1 = T.fr1(s2), b2 = T.fr2(s3), b3 = T.fr3(s0);
         const uint32_t c0 = T.fr0(s2), c1 = T.fr1(s3), c2 = T.fr2(s0), c3 = T.fr3(s1);
@@ -524,96 +509,6 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32
 
 // --------------------------------------------------------------- GHASH ----
 
-// One window pair of a GHASH product (see ghash_mul): windows 2j (low nibble)
-// and 2j+1 (high nibble) of byte j of y, tables of one power at LDS `tab`.
-__device__ __forceinline__ u32x4 ghash_pair(const uint32_t (&yw)[4], int j, const uint8_t *lds,
-                                            uint32_t tab, u32x4 acc)
-{
-    const int d = j >> 2;
-    const uint32_t sel = 0x0c0c0c00u | (uint32_t)(j & 3);
-    const uint32_t alo = __builtin_amdgcn_perm(0u, (yw[d] << 4) & 0xF0F0F0F0u, sel);
-    const uint32_t ahi = __builtin_amdgcn_perm(0u, yw[d] & 0xF0F0F0F0u, sel);
-    const u32x4 e0 = *(const u32x4 *)(lds + tab + (2 * j) * 256 + alo);
-    const u32x4 e1 = *(const u32x4 *)(lds + tab + (2 * j + 1) * 256 + ahi);
-    return xor3(acc, e0, e1);
-}
-
-// AES-CTR block (as aes_ctr) with the product g = y * H^4 woven into its LDS
-// phases.  The AES rounds are a chain of dependent table reads; the GHASH
-// product of the previous step's accumulator does not depend on them, so
-// each of the first 8 phases also issues 2 of its 16 window pairs.  Every
-// phase issues all of its reads (AES and GHASH) before the first use, then
-// consumes them (sched_barrier between the two halves), so a phase costs one
-// LDS round trip.  tsel: the H^4 entry (ghash_mul_lds).
-template <int NR, class TE>
-__device__ __forceinline__ u32x4 aes_ctr_gh(const CtrCache &c, uint32_t cb, const uint32_t *rk,
-                                            const TE &T, const u32x4 y, const uint8_t *lds,
-                                            uint32_t tsel, u32x4 &g)
-{
-    const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
-    u32x4 ga = {0, 0, 0, 0};
-    u32x4 e[4];
-    // issue window pairs 2p and 2p + 1 (bytes 2p, 2p + 1 of y) of phase p < 8
-    auto gh_issue = [&](int p) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int j = 2 * p + q, d = j >> 2;
-            const uint32_t sel = 0x0c0c0500u | (uint32_t)(j & 3);
-            const uint32_t lo = (yw[d] << 4) & 0xF0F0F0F0u, hi = yw[d] & 0xF0F0F0F0u;
-            e[2 * q] = *(const u32x4 *)(lds + (2 * j) * 256 + __builtin_amdgcn_perm(tsel, lo, sel));
-            e[2 * q + 1] = *(const u32x4 *)(lds + (2 * j + 1) * 256 + __builtin_amdgcn_perm(tsel, hi, sel));
-        }
-    };
-    auto gh_use = [&]() {
-        ga = xor3(ga, e[0], e[1]);
-        ga = xor3(ga, e[2], e[3]);
-        // pin the sum here: IR-level sinking would otherwise move every xor
-        // next to the one use of g and keep all 32 loaded entries live
-        asm volatile("" : "+v"(ga.x), "+v"(ga.y), "+v"(ga.z), "+v"(ga.w));
-    };
-    // phase 0: the counter byte's round-1 lookup
-    const uint32_t x0 = T.t3(rk[3] ^ (cb << 24));
-    gh_issue(0);
-    __builtin_amdgcn_sched_barrier(0);
-    const uint32_t u0 = c.c0 ^ x0;
-    gh_use();
-    __builtin_amdgcn_sched_barrier(0);
-    // phase 1: round 2's four lookups of u0
-    const uint32_t v0 = T.t0(u0), v1 = T.t3(u0), v2 = T.t2(u0), v3 = T.t1(u0);
-    gh_issue(1);
-    __builtin_amdgcn_sched_barrier(0);
-    uint32_t s0 = c.d0 ^ v0, s1 = c.d1 ^ v1, s2 = c.d2 ^ v2, s3 = c.d3 ^ v3;
-    gh_use();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int r = 3; r < NR; ++r) {
-        const uint32_t *k = rk + 4 * r;
-        const uint32_t a0 = T.t0(s0), a1 = T.t1(s1), a2 = T.t2r(s2), a3 = T.t3r(s3);
-        const uint32_t b0 = T.t0(s1), b1 = T.t1(s2), b2 = T.t2r(s3), b3 = T.t3r(s0);
-        const uint32_t c0 = T.t0(s2), c1 = T.t1(s3), c2 = T.t2r(s0), c3 = T.t3r(s1);
-        const uint32_t d0 = T.t0(s3), d1 = T.t1(s0), d2 = T.t2r(s1), d3 = T.t3r(s2);
-        if (r - 1 < 8) gh_issue(r - 1);
-        __builtin_amdgcn_sched_barrier(0);
-        s0 = xor3(a0, a1, rotl(xor3(a2, a3, k[0]), 16));
-        s1 = xor3(b0, b1, rotl(xor3(b2, b3, k[1]), 16));
-        s2 = xor3(c0, c1, rotl(xor3(c2, c3, k[2]), 16));
-        s3 = xor3(d0, d1, rotl(xor3(d2, d3, k[3]), 16));
-        if (r - 1 < 8) gh_use();
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // the pairs ride on phases 0..7 (rounds 3..8 are phases 2..7)
-    static_assert(NR >= 9, "GHASH pairs must fit the AES phases");
-    g = ga;
-    const uint32_t *k = rk + 4 * NR;
-    const uint32_t a0 = T.f0(s0), a1 = T.f1(s1), a2 = T.f2(s2), a3 = T.f3(s3);
-    const uint32_t b0 = T.f0(s1), b1 = T.f1(s2), b2 = T.f2(s3), b3 = T.f3(s0);
-    const uint32_t c0 = T.f0(s2), c1 = T.f1(s3), c2 = T.f2(s0), c3 = T.f3(s1);
-    const uint32_t d0 = T.f0(s3), d1 = T.f1(s0), d2 = T.f2(s1), d3 = T.f3(s2);
-    __builtin_amdgcn_sched_barrier(0);
-    return u32x4{(a0 | a1 | a2 | a3) ^ k[0], (b0 | b1 | b2 | b3) ^ k[1], (c0 | c1 | c2 | c3) ^ k[2],
-                 (d0 | d1 | d2 | d3) ^ k[3]};
-}
-
 // x * H^p using the 32 windowed tables of power p at LDS byte offset `tab`.
 // Entry address = tab + w*256 + v*16: the w*256 part folds into the ds_read
 // immediate; (word & 0xF0F0F0F0) already holds high-nibble*16 per byte.
@@ -635,71 +530,6 @@ __device__ __forceinline__ u32x4 ghash_mul(u32x4 x, const uint8_t *lds, uint32_t
             uint32_t ahi = __builtin_amdgcn_perm(0u, hi, sel);
             u32x4 e0 = *(const u32x4 *)(lds + tab + wlo * 256 + alo);
             u32x4 e1 = *(const u32x4 *)(lds + tab + whi * 256 + ahi);
-            acc = xor3(acc, e0, e1);
-        }
-    }
-    return acc;
-}
-
-#ifndef QPP_GHASH_GROUP
-#define QPP_GHASH_GROUP 1
-#endif
-// issue grouping of ghash_mul_lds: input words per group (1 or 2), 0 = the
-// compiler's own schedule (A/B switch)
-constexpr int kGhashGroup = QPP_GHASH_GROUP;
-
-// x * H^p with the table of one power chosen at run time among the
-// workgroup's resident tables: tables of 8 KiB at LDS offsets r * 8192 from
-// `base` (r < 8); tsel = r * 8192.  The table offset rides in byte 1 of the
-// same v_perm that extracts the nibble, so the selection costs no instruction.
-__device__ __forceinline__ u32x4 ghash_mul_lds(u32x4 x, const uint8_t *base, uint32_t tsel)
-{
-    if constexpr (kGhashGroup) {
-        // kGhashGroup input words' reads (8 each) per group, all in flight
-        // before the first use (32 VGPRs per word)
-        const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
-        u32x4 e[2][8];
-        auto issue = [&](int d, u32x4 (&o)[8]) {
-            const uint32_t hi = xw[d] & 0xF0F0F0F0u, lo = (xw[d] << 4) & 0xF0F0F0F0u;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int wlo = 2 * (4 * d + b);
-                const uint32_t sel = 0x0c0c0500u | (uint32_t)b;
-                o[2 * b] = *(const u32x4 *)(base + wlo * 256 + __builtin_amdgcn_perm(tsel, lo, sel));
-                o[2 * b + 1] = *(const u32x4 *)(base + (wlo + 1) * 256 + __builtin_amdgcn_perm(tsel, hi, sel));
-            }
-        };
-        u32x4 acc = {0, 0, 0, 0};
-#pragma unroll
-        for (int d = 0; d < 4; d += kGhashGroup) {
-            issue(d, e[0]);
-            if (kGhashGroup > 1) issue(d + 1, e[1]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 8; i += 2) acc = xor3(acc, e[0][i], e[0][i + 1]);
-            if (kGhashGroup > 1) {
-#pragma unroll
-                for (int i = 0; i < 8; i += 2) acc = xor3(acc, e[1][i], e[1][i + 1]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        return acc;
-    }
-    u32x4 acc = {0, 0, 0, 0};
-    uint32_t xw[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        uint32_t hi = xw[d] & 0xF0F0F0F0u;
-        uint32_t lo = (xw[d] << 4) & 0xF0F0F0F0u;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int wlo = 2 * (4 * d + b), whi = wlo + 1;
-            // byte 0: nibble * 16 (byte b of lo / hi), byte 1: tsel byte 1
-            const uint32_t sel = 0x0c0c0500u | (uint32_t)b;
-            uint32_t alo = __builtin_amdgcn_perm(tsel, lo, sel);
-            uint32_t ahi = __builtin_amdgcn_perm(tsel, hi, sel);
-            u32x4 e0 = *(const u32x4 *)(base + wlo * 256 + alo);
-            u32x4 e1 = *(const u32x4 *)(base + whi * 256 + ahi);
             acc = xor3(acc, e0, e1);
         }
     }
@@ -748,19 +578,15 @@ struct Gh5Grp {
     }
 };
 
-#ifndef QPP_GHASH5_PIPE
-#define QPP_GHASH5_PIPE 1
-#endif
-// Six groups software-pipelined (QPP_GHASH5_PIPE): group g + 1's reads are
-// in flight while group g is summed, so a multiply pays about one LDS round
-// trip instead of one per group; at most two groups' reads (<= 40 VGPRs)
-// are held.  0: four groups, each drained before the next is issued.
+// Six groups software-pipelined: group g + 1's reads are in flight while
+// group g is summed, so a multiply pays about one LDS round trip instead of
+// one per group; at most two groups' reads (<= 40 VGPRs) are held.
 __device__ __forceinline__ u32x4 ghash_mul_lds5(u32x4 x, const uint8_t *base, uint32_t tsel)
 {
     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
     u32x4 acc = {0, 0, 0, 0};
 #define QPP_SB() __builtin_amdgcn_sched_barrier(0)
-    if constexpr (QPP_GHASH5_PIPE) {
+    {
         Gh5Grp<0, 5> a;
         Gh5Grp<5, 9> b;
         Gh5Grp<9, 14> c;
@@ -790,63 +616,15 @@ __device__ __forceinline__ u32x4 ghash_mul_lds5(u32x4 x, const uint8_t *base, ui
         QPP_SB();
         f.consume(acc);
         QPP_SB();
-    } else {
-        Gh5Grp<0, 7> a;
-        Gh5Grp<7, 13> b;
-        Gh5Grp<13, 20> c;
-        Gh5Grp<20, kGh5Windows> d;
-        a.issue(xw, base, tsel);
-        QPP_SB();
-        a.consume(acc);
-        QPP_SB();
-        b.issue(xw, base, tsel);
-        QPP_SB();
-        b.consume(acc);
-        QPP_SB();
-        c.issue(xw, base, tsel);
-        QPP_SB();
-        c.consume(acc);
-        QPP_SB();
-        d.issue(xw, base, tsel);
-        QPP_SB();
-        d.consume(acc);
-        QPP_SB();
     }
 #undef QPP_SB
     return acc;
 }
 
-// x * H^4 with the workgroup's LDS table entry at tsel (layout by QPP_GHASH5)
+// x * H^4 with the workgroup's LDS table entry at tsel
 __device__ __forceinline__ u32x4 ghash_mul_h4(u32x4 x, const uint8_t *base, uint32_t tsel)
 {
-    if constexpr (QPP_GHASH5) return ghash_mul_lds5(x, base, tsel);
-    else return ghash_mul_lds(x, base, tsel);
-}
-
-// The same, one input word (8 reads, 32 VGPRs in flight) at a time: for the
-// multiplies outside the step loop, where all 32 reads in flight would not
-// fit beside the live packet state.
-__device__ __forceinline__ u32x4 ghash_mul_lds_narrow(u32x4 x, const uint8_t *base, uint32_t tsel)
-{
-    u32x4 acc = {0, 0, 0, 0};
-    uint32_t xw[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll 1
-    for (int d = 0; d < 4; ++d) {
-        const uint32_t wd = d == 0 ? xw[0] : d == 1 ? xw[1] : d == 2 ? xw[2] : xw[3];
-        uint32_t hi = wd & 0xF0F0F0F0u;
-        uint32_t lo = (wd << 4) & 0xF0F0F0F0u;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int wlo = 2 * (4 * d + b), whi = wlo + 1;
-            const uint32_t sel = 0x0c0c0500u | (uint32_t)b;
-            uint32_t alo = __builtin_amdgcn_perm(tsel, lo, sel);
-            uint32_t ahi = __builtin_amdgcn_perm(tsel, hi, sel);
-            u32x4 e0 = *(const u32x4 *)(base + wlo * 256 + alo);
-            u32x4 e1 = *(const u32x4 *)(base + whi * 256 + ahi);
-            acc = xor3(acc, e0, e1);
-        }
-    }
-    return acc;
+    return ghash_mul_lds5(x, base, tsel);
 }
 
 // x * H^p from the slot's tables in global memory (tab = that power's 8 KiB):

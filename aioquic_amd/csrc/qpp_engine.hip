@@ -40,43 +40,14 @@ constexpr int kSetupWG = 256;
 // bytes [0, 16) (the first header block) for the header write.
 constexpr int kScratch = 112;
 constexpr int kScrTail = 32, kScrEj0 = 48, kScrPark = 64, kScrHdr = 96;
-constexpr int kStageBytes = 64 * 16;  // one 16-byte block per lane of a wave
 constexpr uint32_t kNoSlot = 0xffffffffu;
 // Descriptor flag set by the host session for a descriptor whose extents do
 // not fit the caller's buffers: the packet reports QPP_S_LENGTH and no byte
 // of it is read or written.
 constexpr uint32_t kFlagReject = 0x8000u;
-#ifndef QPP_STORE_CPOL
-#define QPP_STORE_CPOL 0  // cache policy of the GCM step stores (gfx950: 1 sc0, 2 nt, 16 sc1)
-#endif
-#ifndef QPP_STAGE_LDS
-#define QPP_STAGE_LDS 0  // GCM step input: 1 = LDS-DMA staging buffers, 0 = register prefetch
-#endif
-#ifndef QPP_FUSE_GH
-#define QPP_FUSE_GH 0  // GCM step: GHASH product woven into the AES phases (aes_ctr_gh; measured -2.5 %)
-#endif
-constexpr bool kFuseGh = QPP_FUSE_GH;
-#ifndef QPP_CHACHA_WPE
-#define QPP_CHACHA_WPE 4  // ChaCha20-Poly1305: minimum waves per SIMD (4: 128 VGPRs, 8 spilled; r2i same box vs 1 (146 VGPRs, 3 waves): 64Ki +4 %, 1Mi +1 %, config 5 +1 %)
-#endif
-#ifndef QPP_GCM_PRIO
-#define QPP_GCM_PRIO 0  // study: s_setprio 1 over each step's GHASH phase (1) or AES phase (2)
-#endif
-#ifndef QPP_GCM_PF
-#define QPP_GCM_PF 1  // GCM step input: register prefetch distance in steps (2: BPL 1 same time, BPL 2 -0.6 % with 2-4 VGPRs spilled; r2k)
-#endif
-#ifndef QPP_GCM_ABL
-#define QPP_GCM_ABL 0  // ablation study only (wrong output): step loop without 1 stores, 2 loads, 4 GHASH, 8 AES
-#endif
-#ifndef QPP_CHACHA_ABL
-#define QPP_CHACHA_ABL 0  // ablation study only (wrong output): 1 no payload stores, 2 no payload loads, 4 no Poly1305 in the chunk loop
-#endif
-#ifndef QPP_CHACHA_STAGE
-#define QPP_CHACHA_STAGE 1  // ChaCha20-Poly1305: coalesced loads / stores through LDS staging (0: per-lane chunks)
-#endif
-#ifndef QPP_CHACHA_PREFETCH
-#define QPP_CHACHA_PREFETCH 1  // ChaCha20-Poly1305: next chunk input in registers one unit ahead
-#endif
+// ChaCha20-Poly1305: minimum waves per SIMD (4: 128 VGPRs, 8 spilled; r2i
+// same box against 1 (146 VGPRs, 3 waves): 64 Ki +4 %, 1 Mi +1 %, config 5 +1 %)
+constexpr int kChachaWpe = 4;
 
 // ChaCha20-Poly1305 per-wave LDS staging: at step k a quad works on 4
 // consecutive 64-byte chunks of its packet (lane j: chunk 4k - 1 + j).  Its
@@ -89,9 +60,7 @@ constexpr int kChStage = 4 * kChRegion;
 
 template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
-#if QPP_CHACHA_STAGE
     uint8_t stage[WG / 64][kChStage];
-#endif
     uint8_t scratch[WG / 4][kScratch];
 };
 
@@ -542,7 +511,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                                             const uint8_t *te, const Bufs &B,
                                             const uint8_t *src, uint32_t ioff, uint32_t ooff,
                                             const u32x4 hmask, const uint32_t hbits, const u32x4 h0,
-                                            uint8_t *stage, u32x4 &got_tag)
+                                            u32x4 &got_tag)
 {
     const LdsTe T{te, (lane_fresh() & 31) * 4};
     const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
@@ -594,13 +563,8 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         const bool is_ct = i >= 0 && 16 * i < clen;
         const LdsTe Tl{te, (lane_fresh() & 31) * 4};
         const uint32_t cb = is_ct ? (uint32_t)(i + 2) : 1u;
-        // fused: the previous accumulator's H^4 product rides on this block's
-        // AES phases (A_k = A_{k-1} H^4 + x_k; the first step has no product)
-        u32x4 g = {0, 0, 0, 0};
-        u32x4 ksb;
-        if constexpr (QPP_GCM_ABL & 8) ksb = u32x4{cb, cc.c0, cc.d0, cc.d1};
-        else if constexpr (!kFuseGh || first) ksb = aes_ctr<NR>(cc, cb, rk, Tl);
-        else ksb = aes_ctr_gh<NR>(cc, cb, rk, Tl, acc, G.lds, t4, g);
+        (void)first;
+        const u32x4 ksb = aes_ctr<NR>(cc, cb, rk, Tl);
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
         uint32_t soff = kOob;
         if (is_ct) {
@@ -623,17 +587,12 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
             *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
         }
-        if (!(QPP_GCM_ABL & 1) || out.x == 0x12345678u)
-            __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
-        if constexpr (kFuseGh) {
-            acc = (first ? acc : g) ^ x;
-        } else {
-            acc ^= x;
-            __builtin_amdgcn_sched_barrier(0);
-            // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
-            // is applied after the loop
-            if (!last && !(QPP_GCM_ABL & 4)) acc = ghash_mul_h4(acc, G.lds, t4);
-        }
+        __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, 0);
+        acc ^= x;
+        __builtin_amdgcn_sched_barrier(0);
+        // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
+        // is applied after the loop
+        if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
     };
     // buffer offset of CT block i's input (or out of range)
     auto ct_load = [&](int i) -> uint32_t {
@@ -665,8 +624,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
             *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
         }
-        if (!(QPP_GCM_ABL & 1) || out.x == 0x12345678u)
-            __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, QPP_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, 0);
         return x;
     };
     // BPL = 2: lane blocks i and i + 4 (CT indices) in one step
@@ -676,11 +634,7 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         const uint32_t cb0 = (i >= 0 && 16 * i < clen) ? (uint32_t)(i + 2) : 1u;
         const uint32_t cb1 = (i + 4 >= 0 && 16 * (i + 4) < clen) ? (uint32_t)(i + 6) : 1u;
         u32x4 ks0, ks1;
-        if constexpr (QPP_GCM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
-        if constexpr (QPP_GCM_ABL & 8) {
-            ks0 = u32x4{cb0, cc.c0, cc.d0, cc.d1};
-            ks1 = u32x4{cb1, cc.c0, cc.d0, cc.d1};
-        } else if (first && pad >= 4) {
+        if (first && pad >= 4) {
             // the quad's first four positions are all front padding: only
             // the second block of the first step is real
             ks0 = zero4();
@@ -688,7 +642,6 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         } else {
             aes_ctr2<NR>(cc, cb0, cb1, rk, Tl, ks0, ks1);
         }
-        if constexpr (QPP_GCM_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         u32x4 x0 = blk_out(i, ks0, raw0);
         u32x4 x1 = blk_out(i + 4, ks1, raw1);
         if constexpr (first) {
@@ -697,16 +650,10 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             if (i + 4 == -1) x1 ^= z;
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (QPP_GCM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-        if constexpr (!(QPP_GCM_ABL & 4)) {
-            // (0 ^ 0) H^4 = 0 over front padding
-            if (first && pad >= 4) acc = x1;
-            else acc = ghash_mul_h4(acc ^ x0, G.lds, t4) ^ x1;
-            if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
-        } else {
-            acc ^= x0 ^ x1;
-        }
-        if constexpr (QPP_GCM_PRIO != 0) __builtin_amdgcn_s_setprio(0);
+        // (0 ^ 0) H^4 = 0 over front padding
+        if (first && pad >= 4) acc = x1;
+        else acc = ghash_mul_h4(acc ^ x0, G.lds, t4) ^ x1;
+        if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
     };
 
     got_tag = u32x4{0, 0, 0, 0};
@@ -721,42 +668,15 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
             // step the first of them is the received tag (unprotect)
             u32x4 nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i), 0, 0);
             u32x4 nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i + 4), 0, 0);
-#if QPP_GCM_PF >= 2
-            // two steps ahead (A/B switch): the loads of the step with `rem`
-            // steps left, starting at CT block j (rem 0: the received tag)
-            auto load_for = [&](int rem, int j, u32x4 &a, u32x4 &b) {
-                const uint32_t l0 = rem >= 1 ? ct_load(j) : (rem == 0 && !ENC) ? cin + (uint32_t)clen : kOob;
-                const uint32_t l1 = rem >= 1 ? ct_load(j + 4) : kOob;
-                a = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)l0, 0, 0);
-                b = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)l1, 0, 0);
-            };
-            u32x4 nxt2, nxt3;
-            load_for(S - 1, i + 8, nxt2, nxt3);
-            QPP_PROBE_AT(4);
             auto one2 = [&](int k, auto first_c) {
                 const u32x4 raw0 = nxt0, raw1 = nxt1;
-                nxt0 = nxt2;
-                nxt1 = nxt3;
-                load_for(k - 2, i + 16, nxt2, nxt3);
+                const uint32_t l0 = (!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 8);
+                nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)l0, 0, 0);
+                nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i + 12), 0, 0);
                 step2(i, k == 1, raw0, raw1, first_c);
                 i += 8;
             };
-#else
             QPP_PROBE_AT(4);
-            auto one2 = [&](int k, auto first_c) {
-                const u32x4 raw0 = nxt0, raw1 = nxt1;
-                if constexpr (QPP_GCM_ABL & 2) {
-                    nxt0 = u32x4{(uint32_t)k, 0, 0, 0};
-                    nxt1 = nxt0;
-                } else {
-                    const uint32_t l0 = (!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 8);
-                    nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)l0, 0, 0);
-                    nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i + 12), 0, 0);
-                }
-                step2(i, k == 1, raw0, raw1, first_c);
-                i += 8;
-            };
-#endif
             // the first step is peeled: it alone may carry Z
             one2(S, std::true_type{});
 #pragma unroll 1
@@ -772,59 +692,18 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     } else {
         int i = sub - q;
         // one step: this step's input block, the next step's load (on the
-        // last step the received tag), the block.  The first step is peeled
-        // (no GHASH product to weave in).
-#if QPP_STAGE_LDS
-        // LDS-DMA staging: lane l's 16 bytes land at stage[buf][16 l]
-        auto dma = [&](uint32_t off, int buf) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                B.in, (__attribute__((address_space(3))) void *)(stage + buf * kStageBytes), 16,
-                off, 0, 0, 0);
-        };
-        int b = 0;
-        dma(ct_load(i), 0);
-        QPP_PROBE_AT(4);
-        auto one = [&](int k, auto first_c) {
-            // the compiler does not track LDS-DMA: retire it explicitly (this
-            // also waits for the previous step's store)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const u32x4 raw = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
-            dma((!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 4), b ^ 1);
-            step(i, k == 1, first_c, raw);
-            i += 4;
-            b ^= 1;
-        };
-        one(S, std::true_type{});
-#pragma unroll 1
-        for (int k = S - 1; k > 0; --k) one(k, std::false_type{});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (!ENC) got_tag = *(const u32x4 *)(stage + b * kStageBytes + lane_fresh() * 16);
-#else
-        // register prefetch, one step ahead (4 VGPRs; the compiler counts
-        // vmcnt, so the previous step's store stays in flight)
-        (void)stage;
-        // the input of the step after step k (counting down to 1; step 0 is
+        // last step the received tag), the block.  Register prefetch, one
+        // step ahead (4 VGPRs; the compiler counts vmcnt, so the previous
+        // step's store stays in flight).  The input of the step after step k (counting down to 1; step 0 is
         // the received tag of an unprotect), block j = i + 4 (S - k)
         auto in_of = [&](int k, int j) -> uint32_t {
             return (!ENC && k == 0) ? cin + (uint32_t)clen : ct_load(j);
         };
         u32x4 nxt = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i), 0, 0);
-#if QPP_GCM_PF >= 2
-        // two steps ahead: a step's LDS work (~3 us per wave at 16 waves/CU)
-        // is shorter than a loaded HBM read
-        u32x4 nxt2 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)in_of(S - 1, i + 4), 0, 0);
-#endif
         QPP_PROBE_AT(4);
         auto one = [&](int k, auto first_c) {
             const u32x4 raw = nxt;
-#if QPP_GCM_PF >= 2
-            nxt = nxt2;
-            if constexpr (QPP_GCM_ABL & 2) nxt2 = u32x4{(uint32_t)k, 0, 0, 0};
-            else nxt2 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)(k >= 2 ? in_of(k - 2, i + 8) : kOob), 0, 0);
-#else
-            if constexpr (QPP_GCM_ABL & 2) nxt = u32x4{(uint32_t)k, 0, 0, 0};
-            else nxt = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)in_of(k - 1, i + 4), 0, 0);
-#endif
+            nxt = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)in_of(k - 1, i + 4), 0, 0);
             step(i, k == 1, first_c, raw);
             i += 4;
         };
@@ -832,7 +711,6 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
 #pragma unroll 1
         for (int k = S - 1; k > 0; --k) one(k, std::false_type{});
         if (!ENC) got_tag = nxt;
-#endif
     }
     QPP_PROBE_AT(5);
     // lane-derived values recomputed after the loop rather than kept (spilled)
@@ -888,7 +766,6 @@ __device__ __forceinline__ uint32_t quad_dpp(uint32_t v)
 {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
-constexpr int kQuadBcast3 = 0xFF;  // quad_perm [3,3,3,3]
 
 // values the compiler must not keep live across the chunk loop: pass them
 // through an empty asm so powers of r are recomputed after it
@@ -899,7 +776,6 @@ __device__ __forceinline__ P130 launder(P130 x)
     return x;
 }
 
-#if QPP_CHACHA_STAGE
 // 16 bytes per lane from buffer offset `off` (out of range: zeros) into LDS at
 // lds + 16 * lane (LDS-DMA)
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds, uint32_t off)
@@ -1088,166 +964,6 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         }
     }
 }
-#else
-template <bool ENC>
-__device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr)
-{
-    const uint32_t *key = ks->rk;
-    const uint32_t n0 = P.nonce.x, n1 = P.nonce.y, n2 = P.nonce.z;
-    const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4;
-    const int n_g = n_a + n_c + 1;
-    const int chunks = (P.clen + 63) >> 6;
-    const bool unmask = !ENC && P.hp;
-    const uint8_t *pin = P.src + P.hlen;
-    uint8_t *pout = P.dst + P.hlen;
-    // end of the readable input region (protect: header + payload; unprotect:
-    // + tag): partial blocks are loaded end-aligned within it (ld_win)
-    const int rlen = P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN);
-    // input bytes [0, 16) parked by k_chacha (absent below 16 bytes)
-    const uint8_t *h0 = rlen >= 16 ? scr + kScrHdr : nullptr;
-
-    // the 64 input bytes of chunk c
-    auto fetch = [&](int c, u32x4 (&v)[4]) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int i = 4 * c + t;
-            v[t] = (c >= 0 && i < n_c && !(QPP_CHACHA_ABL & 2))
-                       ? ld_win(pin + 16 * i, min(16, P.clen - 16 * i), P.src, P.src + rlen)
-                       : u32x4{(uint32_t)i, 0, 0, 0};
-        }
-    };
-    // keystream chunk c: xor, store, and the Poly1305 input blocks (ciphertext)
-    auto crypt = [&](int c, const u32x4 (&din)[4], const uint32_t (&blk)[16], u32x4 (&x)[4]) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int i = 4 * c + t;
-            x[t] = u32x4{0, 0, 0, 0};
-            if (i >= n_c) continue;
-            const int nb = min(16, P.clen - 16 * i);
-            const u32x4 dout = din[t] ^ u32x4{blk[4 * t], blk[4 * t + 1], blk[4 * t + 2], blk[4 * t + 3]};
-            if (!(QPP_CHACHA_ABL & 1)) st_part(pout + 16 * i, dout, nb);
-            else if (dout.x == 0x12345678u) st16(pout, dout);
-            x[t] = keep_bytes(ENC ? dout : din[t], nb);
-            if (ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[t];
-        }
-    };
-
-    // ---- unit 0..3: chunks 0-2 on lanes 0-2, the one-time key on lane 3
-    const int c0 = sub < 3 ? sub : -1;
-    u32x4 cur[4], x[4];
-    fetch(c0 < chunks ? c0 : -1, cur);
-    uint32_t blk[16];
-    chacha_block(key, sub == 3 ? 0u : (uint32_t)(1 + sub), n0, n1, n2, blk);
-    uint32_t kw[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) kw[w] = quad_dpp<kQuadBcast3>(blk[w]);
-    // s waits in LDS until the tag (scratch [64, 80): unused by this suite)
-    *(u32x4 *)(scr + 64) = u32x4{kw[4], kw[5], kw[6], kw[7]};
-    const P130 r = p130_r(kw[0], kw[1], kw[2], kw[3]);
-    if (c0 >= 0 && c0 < chunks) crypt(c0, cur, blk, x);
-
-#if QPP_CHACHA_PREFETCH
-    // next unit's input, fetched one unit ahead
-    u32x4 nxt[4];
-    fetch(3 + sub < chunks ? 3 + sub : -1, nxt);
-#endif
-
-    P130 acc = p130_zero();
-    int g_last = -1;
-    // lane 0 starts its chain with the associated data
-    if (sub == 0) {
-        for (int g = 0; g < n_a; ++g) {
-            const int nb = min(16, P.hlen - 16 * g);
-            u32x4 a = (g == 0 && h0) ? keep_bytes(*(const u32x4 *)h0, nb)
-                                     : ld_win(P.src + 16 * g, nb, P.src, P.src + rlen);
-            if (unmask) a ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
-            if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
-            acc = p130_mul(p130_add(acc, p130_block(a)), r);
-            g_last = g;
-        }
-    }
-    if (c0 >= 0 && c0 < chunks) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (4 * c0 + t >= n_c) break;
-            acc = p130_mul(p130_add(acc, p130_block(x[t])), r);
-            g_last = n_a + 4 * c0 + t;
-        }
-    }
-    P130 r12;
-    {
-        const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
-        r12 = p130_mul(r8, r4);
-        // the first jump of lanes 0-2 skips the 2 chunks between theirs (r^8)
-        if (sub < 3 && g_last >= 0 && 3 + sub < chunks) acc = p130_mul(acc, r8);
-    }
-    // ---- units 4k + sub, k >= 1: chunk 4k + sub - 1; later jumps skip 3 chunks (r^12)
-    bool first = true;
-    for (int c = 3 + sub; c < chunks; c += 4) {
-#if QPP_CHACHA_PREFETCH
-#pragma unroll
-        for (int t = 0; t < 4; ++t) cur[t] = nxt[t];
-        fetch(c + 4 < chunks ? c + 4 : -1, nxt);
-#else
-        // issued ahead of the block function, which hides their latency
-        fetch(c, cur);
-#endif
-        chacha_block(key, (uint32_t)(1 + c), n0, n1, n2, blk);
-        crypt(c, cur, blk, x);
-        if (!first && g_last >= 0 && !(QPP_CHACHA_ABL & 4)) acc = p130_mul(acc, r12);
-        first = false;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (4 * c + t >= n_c) break;
-            if (!(QPP_CHACHA_ABL & 4)) acc = p130_mul(p130_add(acc, p130_block(x[t])), r);
-            else acc.v[t] ^= x[t].x;
-            g_last = n_a + 4 * c + t;
-        }
-    }
-    // acc = sum m_g r^(g_last - g + 1); scale to r^(n_g - g) with r^(n_g - 1 - g_last)
-    int e = n_g - 1 - g_last;  // >= 1 when this lane holds blocks
-    if (g_last < 0) e = 0;
-    P130 f = acc;
-    if (e > 1) {
-        // square-and-multiply over r^1, r^2, r^4, r^8, r^16 (e <= 17), powers
-        // recomputed here rather than kept through the loop
-        const P130 rr = launder(r);
-        const P130 r2 = p130_mul(rr, rr), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
-        const int m = e - 1;
-        if (m & 1) f = p130_mul(f, rr);
-        if (m & 2) f = p130_mul(f, r2);
-        if (m & 4) f = p130_mul(f, r4);
-        if (m & 8) f = p130_mul(f, r8);
-        if (m & 16) f = p130_mul(f, p130_mul(r8, r8));
-    }
-    // sum over the quad (limbs < 2^28 each, no carries needed), add the lengths block
-    P130 sum;
-#pragma unroll
-    for (int l = 0; l < 5; ++l) {
-        uint32_t v = f.v[l];
-        v += quad_perm<kQuadSwap1>(v);
-        v += quad_perm<kQuadSwap2>(v);
-        sum.v[l] = v;
-    }
-    const u32x4 lens = u32x4{(uint32_t)P.hlen, 0u, (uint32_t)P.clen, 0u};
-    sum = p130_mul(p130_add(sum, p130_block(lens)), r);
-    const u32x4 sw = *(const u32x4 *)(scr + 64);
-    const u32x4 tag = p130_finish(sum, sw.x, sw.y, sw.z, sw.w);
-    if (ENC) {
-        if (sub == 0) st16(pout + P.clen, tag);
-        if (P.hp) protect_finish_hp<QPP_CHACHA20_POLY1305>(P, ks, sub, scr, tag, ConstTe{}, h0);
-    } else {
-        const u32x4 got = ld16(pin + P.clen);
-        const u32x4 diff = got ^ tag;
-        if ((diff.x | diff.y | diff.z | diff.w) != 0) {
-            P.status = QPP_S_DECRYPT;
-            // chunk c (blocks 4c..4c+3) is unit c (c < 3) or c + 1 of the quad
-            wipe_payload(P, sub, [&](int i) { const int c = i >> 2; return c < 3 ? c : (c + 1) & 3; });
-        }
-    }
-}
-
-#endif  // QPP_CHACHA_STAGE
 
 template <bool ENC>
 __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int sub, const Pkt &P)
@@ -1288,19 +1004,15 @@ __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int su
 // slots in order, so the 16 waves hold one or two slots at a time.
 constexpr int kTabEntries = 4;
 static_assert(kGhLdsEntry % 1024 == 0, "LDS-DMA pieces of 1 KiB");
-static_assert(!(QPP_GHASH5 && QPP_FUSE_GH), "the fused GHASH phases read the 4-bit layout");
 
 template <int WG>
 struct __attribute__((aligned(16))) GcmSmem {
     // GHASH table entries first (LDS offset 0: ghash_mul_lds adds e * 8 KiB in
     // its v_perm), then the AES image at 32 KiB; both within the 16-bit
     // ds_read immediate range
-    uint8_t h4[kTabEntries][kGhLdsEntry];     // 56 KiB (QPP_GHASH5) or 32 KiB
+    uint8_t h4[kTabEntries][kGhLdsEntry];     // 56 KiB
     uint8_t te[kTeBytes];                     // Te0|Te1 x 32 bank copies   64 KiB
     uint8_t scratch[WG / 4][kScratch];
-#if QPP_STAGE_LDS
-    uint8_t stage[WG / 64][2][kStageBytes];   // per-wave LDS-DMA input staging
-#endif
     uint32_t eslot[kTabEntries];              // slot held by entry e (kNoSlot: none)
     uint32_t eref[kTabEntries];               // waves running entry e's slot
     uint32_t eready[kTabEntries];             // entry e's table has landed
@@ -1366,8 +1078,8 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
     }
     if (e == kNoSlot) return e;  // watchdog: no entry came free (the slot's packets are skipped)
     if (load) {
-        // H^4 of the slot in the step loop's layout: 13 (or 8) pieces of 1 KiB
-        const uint8_t *src = gtab + (size_t)cur * kGhashTabBytes + (QPP_GHASH5 ? kGh5Off : 3 * kGhashPowBytes);
+        // H^4 of the slot in the step loop's layout: 14 pieces of 1 KiB
+        const uint8_t *src = gtab + (size_t)cur * kGhashTabBytes + kGh5Off;
         const uint32_t l = lane_fresh();
 #pragma unroll
         for (int c = 0; c < kGhLdsEntry / 1024; ++c)
@@ -1508,11 +1220,6 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
                     const u32x4 tag = gcm_packet<kNR, ENC, BPL>(
                         P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
                         (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0,
-#if QPP_STAGE_LDS
-                        sm.stage[wv][0],
-#else
-                        nullptr,
-#endif
                         got_tag);
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
@@ -1606,7 +1313,7 @@ __device__ __forceinline__ WaveSpan wave_span(uint32_t n, const uint32_t *items,
 // ChaCha20-Poly1305: no tables, so every wave runs its packets slot by slot
 // on its own, with the keys read from the slot (scalar loads).
 template <bool ENC, int WG>
-__global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__restrict__ slots,
+__global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__restrict__ slots,
                                                              uint32_t cap,
                                                              const qpp_desc *__restrict__ desc,
                                                              uint32_t n, const uint8_t *gin,
@@ -1621,11 +1328,9 @@ __global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__
     const uint32_t lim = W.e, planned = irange != nullptr;
     __shared__ ChachaSmem<WG> sm;
     const uint32_t t1 = threadIdx.x, p1 = W.b + ((t1 & 63) >> 2);
-#if QPP_CHACHA_STAGE
     // 32-bit buffer views based at the wave's lowest input / output offsets
     // (a wave's packets must lie within 4 GiB of each other, as for GCM)
     uint64_t bi, bo;
-#endif
     {
         uint64_t in0 = ~0ull, out0 = ~0ull;
         if (p1 < lim) {
@@ -1634,13 +1339,8 @@ __global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__
             out0 = d.out_off;
             if (d.slot >= cap && (t1 & 3) == 0) res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
         }
-#if QPP_CHACHA_STAGE
         bi = wave_min_u64(in0);
         bo = wave_min_u64(out0);
-#else
-        (void)in0;
-        (void)out0;
-#endif
     }
     // slot by slot among the wave's packets, lowest first (usually one); the
     // descriptor is re-read each time rather than kept live (VGPRs)
@@ -1666,24 +1366,18 @@ __global__ __launch_bounds__(WG, QPP_CHACHA_WPE) void k_chacha(const KeySlot *__
             // lane-derived values from a fresh lane id: derived from t1 they
             // would be hoisted out of the loop and held live across it
             const uint32_t tf = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) << 6 | lane_fresh();
-#if QPP_CHACHA_STAGE
             const uint64_t ioff = d.in_off - bi, ooff = d.out_off - bo;
             if (P.status == QPP_S_OK &&
                 (ioff + (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN) > kBufBytes ||
                  ooff + (uint64_t)(P.hlen + P.clen + QPP_TAG_LEN) > kBufBytes))
                 P.status = QPP_S_LENGTH;  // the wave's packets span more than 4 GiB
-#endif
             if (P.status == QPP_S_OK) {
                 *(u32x4 *)(sm.scratch[tf >> 2] + kScrHdr) = pre.h0;
-#if QPP_CHACHA_STAGE
                 const Bufs B{
                     __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
                     __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
                 chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2], sm.stage[tf >> 6], B, (uint32_t)ioff,
                                    (uint32_t)ooff);
-#else
-                chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2]);
-#endif
             }
             write_result<ENC>(res, planned ? desc[p1].rsv : p1, lane_fresh() & 3, P);
         }
@@ -2091,32 +1785,22 @@ int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *st
     return e == hipSuccess ? QPP_OK : QPP_E_HIP;
 }
 
-// Workgroup size per suite family (tuned on MI355X; overridable for sweeps
-// with QPP_WG_GCM / QPP_WG_CHACHA = 512 | 768 | 1024).
+// Workgroup sizes (tuned on MI355X, tools/sweep_wg.sh): GCM 1024 (one
+// persistent workgroup per CU, 4 waves per SIMD), ChaCha20-Poly1305 256.
 static const int kGcmWG = 1024;
-static const int kChachaWGEnc = 256, kChachaWGDec = 256;  // measured: tools/sweep_wg.sh
+static const int kChachaWG = 256;
 
-// workgroup size overrides for experiments (QPP_WG_GCM, QPP_WG_CHACHA_ENC /
-// _DEC); only the sizes instantiated below are accepted
-static int wg_choice(const char *env, int dflt, bool chacha)
-{
-    const char *v = getenv(env);
-    if (!v) return dflt;
-    const int w = atoi(v);
-    if (chacha) return (w == 256 || w == 512 || w == 1024) ? w : dflt;
-    return (w == 512 || w == 768 || w == 1024) ? w : dflt;
-}
-
-// GCM blocks per lane per step (gcm_pad): QPP_GCM_BPL = 1 or 2.  2 (r2i,
-// same box, 2 x 2 runs): north star 1.419 -> 1.389 ms protect (423 -> 435
-// GiB/s), config 4 310 -> 316 GiB/s; WRITE_SIZE 2.08 -> 1.78 GB per 1Mi launch
-static const int kGcmBpl = 2;
+// GCM blocks per lane per step (gcm_pad): 2 (r2i, same box: north star
+// 1.419 -> 1.389 ms protect, config 4 310 -> 316 GiB/s; WRITE_SIZE 2.08 ->
+// 1.78 GB per 1 Mi launch).  QPP_GCM_BPL=1 selects the one-block form (kept
+// under test); read once per process.
 static int gcm_bpl_choice()
 {
-    const char *v = getenv("QPP_GCM_BPL");
-    if (!v) return kGcmBpl;
-    const int b = atoi(v);
-    return (b == 1 || b == 2) ? b : kGcmBpl;
+    static const int b = [] {
+        const char *v = getenv("QPP_GCM_BPL");
+        return (v && atoi(v) == 1) ? 1 : 2;
+    }();
+    return b;
 }
 
 // Persistent GCM grid: one workgroup per CU (the kernel's LDS admits no
@@ -2155,56 +1839,39 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     // planned: each suite's launch covers at most every wave item of the batch
     const uint32_t *d_items = plan ? plan->d_items : nullptr, *d_irange = plan ? plan->d_irange : nullptr;
     const uint32_t waves = plan ? qpp_internal_plan_max_items(n, kt->cap) : (n + 15) / 16;
-    const int wg_gcm = wg_choice("QPP_WG_GCM", kGcmWG, false);
     const int bpl_gcm = gcm_bpl_choice();
-    const int wg_cc = enc ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
-                          : wg_choice("QPP_WG_CHACHA_DEC", kChachaWGDec, true);
-#define QPP_LAUNCH_GCM_WGB(SUITE, WGV, BPLV)                                                   \
+#define QPP_LAUNCH_GCM_B(SUITE, BPLV)                                                          \
     do {                                                                                       \
-        const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
+        const dim3 grid(gcm_grid(waves, kGcmWG / 64)), block(kGcmWG);                           \
         if (enc)                                                                               \
-            hipLaunchKernelGGL((k_gcm<SUITE, true, WGV, BPLV>), grid, block, 0, s, kt->d_slots, \
-                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, d_items,    \
-                               d_irange);                                                      \
+            hipLaunchKernelGGL((k_gcm<SUITE, true, kGcmWG, BPLV>), grid, block, 0, s,          \
+                               kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
+                               d_items, d_irange);                                             \
         else                                                                                   \
-            hipLaunchKernelGGL((k_gcm<SUITE, false, WGV, BPLV>), grid, block, 0, s,            \
+            hipLaunchKernelGGL((k_gcm<SUITE, false, kGcmWG, BPLV>), grid, block, 0, s,         \
                                kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
                                d_items, d_irange);                                             \
     } while (0)
-#define QPP_LAUNCH_GCM_WG(SUITE, WGV)                                                          \
-    do {                                                                                       \
-        if (bpl_gcm == 2) QPP_LAUNCH_GCM_WGB(SUITE, WGV, 2);                                    \
-        else QPP_LAUNCH_GCM_WGB(SUITE, WGV, 1);                                                 \
-    } while (0)
-#define QPP_LAUNCH_CHACHA_WG(WGV)                                                              \
-    do {                                                                                       \
-        const dim3 grid((waves + WGV / 64 - 1) / (WGV / 64)), block(WGV);                      \
-        if (enc)                                                                               \
-            hipLaunchKernelGGL((k_chacha<true, WGV>), grid, block, 0, s, kt->d_slots, kt->cap, \
-                               d_desc, n, d_in, d_out, d_res, d_items, d_irange);              \
-        else                                                                                   \
-            hipLaunchKernelGGL((k_chacha<false, WGV>), grid, block, 0, s, kt->d_slots,         \
-                               kt->cap, d_desc, n, d_in, d_out, d_res, d_items, d_irange);     \
-    } while (0)
 #define QPP_LAUNCH_GCM(SUITE)                                                                  \
     if (mask & (1u << SUITE)) {                                                                \
-        if (wg_gcm == 512) QPP_LAUNCH_GCM_WG(SUITE, 512);                                      \
-        else if (wg_gcm == 768) QPP_LAUNCH_GCM_WG(SUITE, 768);                                 \
-        else QPP_LAUNCH_GCM_WG(SUITE, 1024);                                                   \
+        if (bpl_gcm == 1) QPP_LAUNCH_GCM_B(SUITE, 1);                                           \
+        else QPP_LAUNCH_GCM_B(SUITE, 2);                                                        \
         HIPCHK(hipGetLastError());                                                             \
     }
     QPP_LAUNCH_GCM(QPP_AES_128_GCM)
     QPP_LAUNCH_GCM(QPP_AES_256_GCM)
     if (mask & (1u << QPP_CHACHA20_POLY1305)) {
-        if (wg_cc == 256) QPP_LAUNCH_CHACHA_WG(256);
-        else if (wg_cc == 1024) QPP_LAUNCH_CHACHA_WG(1024);
-        else QPP_LAUNCH_CHACHA_WG(512);
+        const dim3 grid((waves + kChachaWG / 64 - 1) / (kChachaWG / 64)), block(kChachaWG);
+        if (enc)
+            hipLaunchKernelGGL((k_chacha<true, kChachaWG>), grid, block, 0, s, kt->d_slots, kt->cap,
+                               d_desc, n, d_in, d_out, d_res, d_items, d_irange);
+        else
+            hipLaunchKernelGGL((k_chacha<false, kChachaWG>), grid, block, 0, s, kt->d_slots, kt->cap,
+                               d_desc, n, d_in, d_out, d_res, d_items, d_irange);
         HIPCHK(hipGetLastError());
     }
 #undef QPP_LAUNCH_GCM
-#undef QPP_LAUNCH_GCM_WG
-#undef QPP_LAUNCH_GCM_WGB
-#undef QPP_LAUNCH_CHACHA_WG
+#undef QPP_LAUNCH_GCM_B
     return QPP_OK;
 }
 

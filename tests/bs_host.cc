@@ -1,9 +1,9 @@
-// Host build of aioquic_amd/csrc/qpp_bitslice.h for the CPU unit test
+// Host build of tools/bitslice/qpp_bitslice.h for the CPU unit test
 // (tests/test_bitslice.py): 32 blocks per call through the bitsliced path.
 #include <stdint.h>
 #include <string.h>
 
-#include "../aioquic_amd/csrc/qpp_bitslice.h"
+#include "../tools/bitslice/qpp_bitslice.h"
 
 namespace {
 

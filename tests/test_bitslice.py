@@ -1,4 +1,4 @@
-"""CPU check of the bitsliced AES (aioquic_amd/csrc/qpp_bitslice.h, built for
+"""CPU check of the bitsliced AES (tools/bitslice/qpp_bitslice.h, built for
 the host here): the Boyar-Peralta S-box circuit against the FIPS-197 S-box
 for all 256 inputs, the FIPS-197 App. C known answers, and random blocks
 against the oracle's AES-ECB (the header-protection mask of the AES suites,

@@ -1,6 +1,6 @@
 """Map the bitsliced AES round circuit onto gfx950's v_bitop3_b32 (any
 boolean function of three 32-bit operands, at most one of them scalar) and
-emit aioquic_amd/csrc/qpp_bs_gen.h.
+emit tools/bitslice/qpp_bs_gen.h.
 
 The circuit per output column of a round is four S-boxes (the Boyar-Peralta
 depth-16 circuit, as in qpp_bitslice.h) followed by MixColumns.  The round key
@@ -15,7 +15,7 @@ into that consumer; a LUT all of whose consumers can absorb it is duplicated
 into them.  Several merge orders are tried and the smallest cover is kept.
 The result is checked against the unmapped circuit on random inputs.
 
-    python tools/lutmap.py            # writes aioquic_amd/csrc/qpp_bs_gen.h
+    python tools/lutmap.py            # writes tools/bitslice/qpp_bs_gen.h
 """
 
 import os
@@ -23,7 +23,7 @@ import random
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "aioquic_amd", "csrc", "qpp_bs_gen.h")
+OUT = os.path.join(ROOT, "tools", "bitslice", "qpp_bs_gen.h")
 M32 = 0xFFFFFFFF
 
 # ------------------------------------------------------------------ circuit --

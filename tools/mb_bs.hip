@@ -1,4 +1,4 @@
-// Bitsliced AES throughput on one MI355X (qpp_bitslice.h): each lane runs
+// Bitsliced AES throughput on one MI355X (tools/bitslice/qpp_bitslice.h): each lane runs
 // 32 blocks per AES call.  MODE 0: AES only; MODE 1: plus the transposes in
 // and out (slot words <-> planes).  Prints CU-cycles per 16-byte block at the
 // measured clock (s_memtime / s_memrealtime).
@@ -8,7 +8,7 @@
 
 #include <vector>
 
-#include "../aioquic_amd/csrc/qpp_bitslice.h"
+#include "bitslice/qpp_bitslice.h"
 
 __device__ unsigned long long g_clk[8192 * 4];
 #ifndef QPP_MB_WAVES
