@@ -22,7 +22,8 @@ step (quic/connection.py:905-947, CryptoPair.decrypt_packet, crypto.py:184-192).
       does, and a later packet's truncated number is decoded against it.
   A later packet whose outcome could depend on such an update is relaunched.
   A packet decoded under the earlier expected number whose decoded value is
-  unchanged used the same nonce, so its result stands.  Each round resolves at
+  unchanged used the same nonce, so its result stands -- a failed one too
+  (forged or corrupt packets cost no extra launch).  Each round resolves at
   least the first pending packet of every pair, so run() ends after at most
   1 + (state changes) rounds.
   Outcomes are (plain_header, payload, packet_number) tuples or the exception
@@ -32,10 +33,12 @@ step (quic/connection.py:905-947, CryptoPair.decrypt_packet, crypto.py:184-192).
 
 from __future__ import annotations
 
+import weakref
 from typing import Optional, Union
 
 import numpy as np
 
+from . import crypto as crypto_mod
 from . import layout as L
 from ._crypto import CryptoError, KeyTable, protect_list, unprotect_list
 from .crypto import CryptoContext, CryptoPair, KeyUnavailableError, next_key_phase
@@ -49,27 +52,41 @@ class KeySlots:
 
     A slot is keyed by the identity of a context's (AEAD, HeaderProtection,
     key phase).  Those objects are immutable once built, so a slot never goes
-    stale.  Objects are kept alive while slotted, so their ids stay unique.
+    stale.  Objects are kept alive while slotted, so their ids stay unique,
+    until their context lets them go: CryptoContext.teardown and a key update
+    (apply_key_phase) release them here (``release``), which frees the slot
+    and clears its device entry, as the reference drops its EVP contexts.
     When the table is full it is cleared and refilled; that happens only
-    between launches."""
+    between launches.
+
+    Like the reference's AEAD objects, a KeySlots is not meant to be shared
+    by threads; the batched callers' default table is one per thread."""
 
     def __init__(self, capacity: int = 1024) -> None:
         self.capacity = int(capacity)
         self.table = KeyTable(self.capacity)
         self._slot: dict = {}
-        self._keep: list = []
+        self._keep: dict = {}  # slot -> (aead, hp)
+        self._free: list = []
+        self._by_obj: dict = {}  # id(aead or hp) -> idents using it
         self._pending: list = []
+        _holders.add(self)
 
     def slot_for(self, aead, hp, key_phase: int) -> int:
         ident = (id(aead), id(hp), int(key_phase))
         s = self._slot.get(ident)
         if s is not None:
             return s
-        if len(self._slot) >= self.capacity:
+        if self._free:
+            s = self._free.pop()
+        elif len(self._keep) < self.capacity:
+            s = len(self._keep)
+        else:
             raise OverflowError("key table full")
-        s = len(self._slot)
         self._slot[ident] = s
-        self._keep.append((aead, hp))
+        self._keep[s] = (aead, hp)
+        self._by_obj.setdefault(ident[0], []).append(ident)
+        self._by_obj.setdefault(ident[1], []).append(ident)
         suite, key, iv = aead._material()
         _, hp_key = hp._material()
         self._pending.append(L.key_material(s, suite, key, iv, hp_key, key_phase))
@@ -78,6 +95,8 @@ class KeySlots:
     def reset(self) -> None:
         self._slot.clear()
         self._keep.clear()
+        self._free.clear()
+        self._by_obj.clear()
         self._pending.clear()
 
     def commit(self) -> None:
@@ -98,6 +117,35 @@ class KeySlots:
             slots = [self.slot_for(*t) for t in triples]
         self.commit()
         return slots
+
+    def release(self, objs) -> None:
+        """Forget every slot built from one of `objs` (AEAD or HP objects)
+        and clear those device entries."""
+        dropped = set()
+        for o in objs:
+            for k in self._by_obj.pop(id(o), ()) if o is not None else ():
+                s = self._slot.pop(k, None)
+                if s is None:
+                    continue  # already gone through its other object
+                self._keep.pop(s, None)
+                self._free.append(s)
+                dropped.add(s)
+        if not dropped:
+            return
+        self._pending = [m for m in self._pending if int(m["slot"][0]) not in dropped]
+        self.table.clear(np.asarray(sorted(dropped), np.uint32).tobytes())
+
+
+# every live KeySlots, so that a context's teardown can release its keys
+_holders: "weakref.WeakSet[KeySlots]" = weakref.WeakSet()
+
+
+def _release_keys(*objs) -> None:
+    for h in list(_holders):
+        h.release(objs)
+
+
+crypto_mod._KEY_RELEASE_HOOKS.append(_release_keys)
 
 
 def _raise_status(status: int) -> Exception:
@@ -322,23 +370,21 @@ class ReceiveBatch:
                 space = spaces[i]
                 exp_now = space.expected_packet_number
                 moved = exp_now != exp_at[i]
-                if status != L.S_OK:
-                    if moved:
-                        # decoded under an expected number an earlier packet
-                        # has since raised: the packet number, hence the
-                        # nonce, may differ now -- relaunch
-                        blocked.add(id(pair))
-                        stale.append(i)
-                    else:
-                        outcome[i] = _raise_status(status)
-                    continue
                 pn = r_pn[i]
-                if moved:
+                # decoded under an expected number an earlier packet has since
+                # raised: only a packet whose number (hence nonce) decodes
+                # differently now needs another launch.  A failed tag check
+                # reports its number too; length and missing-key failures do
+                # not depend on the expected number at all.
+                if moved and status in (L.S_OK, L.S_DECRYPT):
                     pn_len = r_hl[i] - offs[i]
                     if decode_packet_number(_signed_trunc(pn, pn_len), pn_len * 8, exp_now) != pn:
-                        blocked.add(id(pair))  # decoded under a stale expected number
+                        blocked.add(id(pair))
                         stale.append(i)
                         continue
+                if status != L.S_OK:
+                    outcome[i] = _raise_status(status)
+                    continue
                 out = r_out[i]
                 outcome[i] = (out[0], out[1], pn)
                 if i in rolled_at:

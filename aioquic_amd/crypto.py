@@ -57,6 +57,16 @@ def NoCallback(trigger: str) -> None:
     """Default setup / teardown hook: does nothing."""
 
 
+# called with the AEAD / HP objects a context lets go of (teardown, or the
+# AEAD replaced by a key update), so batch key tables drop them too
+_KEY_RELEASE_HOOKS: list = []
+
+
+def _release(*objs) -> None:
+    for hook in _KEY_RELEASE_HOOKS:
+        hook(*objs)
+
+
 class KeyUnavailableError(CryptoError):
     """No key installed for the packet (decrypt before setup)."""
 
@@ -146,8 +156,10 @@ class CryptoContext:
         self._setup_cb("tls")
 
     def teardown(self) -> None:
+        held = (self.aead, self.hp)
         self._forget()
         self._slots = None
+        _release(*held)
         self._teardown_cb("tls")
 
     def is_valid(self) -> bool:
@@ -195,7 +207,10 @@ class CryptoContext:
 
 def apply_key_phase(self: CryptoContext, crypto: CryptoContext, trigger: str) -> None:
     """Adopt `crypto`'s AEAD key, phase and secret (the HP key is kept)."""
+    old = self.aead
     self.aead, self.key_phase, self.secret = crypto.aead, crypto.key_phase, crypto.secret
+    if old is not None and old is not self.aead:
+        _release(old)
     hook = self._setup_cb
     hook(trigger)
 

@@ -22,6 +22,7 @@ reference's.
 
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass, field
 from enum import Enum
 from typing import Any, Callable, Optional, Sequence
@@ -91,14 +92,17 @@ class _Pending:
     keys: tuple  # (aead, hp, key_phase) of the send context
 
 
-_shared_slots: Optional[KeySlots] = None
+_per_thread = threading.local()
 
 
 def _default_slots() -> KeySlots:
-    global _shared_slots
-    if _shared_slots is None:
-        _shared_slots = KeySlots(4096)
-    return _shared_slots
+    """The builders' default key table: one per OS thread, so concurrent
+    flushes on different threads never assign or reset each other's slots
+    (the C extension gives each thread its own staging the same way)."""
+    t = getattr(_per_thread, "slots", None)
+    if t is None:
+        t = _per_thread.slots = KeySlots(4096)
+    return t
 
 
 class QuicPacketBuilder:

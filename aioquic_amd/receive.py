@@ -20,7 +20,7 @@ RFC 9000 sec. 12.2), no per-packet header parse.
 
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -34,6 +34,7 @@ from .packet import (
     PACKET_LONG_HEADER,
     QuicHeader,
     QuicPacketType,
+    QuicProtocolVersion,
     pull_quic_header,
 )
 from .tls import Epoch
@@ -51,14 +52,17 @@ _EPOCH_OF_TYPE = {
 @dataclass
 class ConnectionKeys:
     """What receive_datagram consults per packet: the crypto pairs per epoch
-    (Initial ones per version), the packet number spaces, the CID length
-    and the role."""
+    (Initial ones per version), the packet number spaces, the CID length,
+    the role and the versions the configuration accepts
+    (QuicConfiguration.supported_versions, configuration.py:115-120)."""
 
     cryptos: Dict[Epoch, Any]
     spaces: Dict[Epoch, Any]
     cryptos_initial: Optional[Dict[int, Any]] = None
     host_cid_length: int = 8
     is_client: bool = False
+    supported_versions: List[int] = field(
+        default_factory=lambda: [QuicProtocolVersion.VERSION_1, QuicProtocolVersion.VERSION_2])
 
     def pair_and_space(self, epoch: Epoch, version: Optional[int]):
         if epoch == Epoch.INITIAL:
@@ -102,8 +106,16 @@ def _walk_long(conn: ConnectionKeys, d: int, data: bytes, batch: ReceiveBatch, o
             out.append(ReceivedPacket(d, start, header, ptype, Epoch.INITIAL,
                                       dropped="initial_packet_datagram_too_small"))
             return
-        if ptype in (QuicPacketType.VERSION_NEGOTIATION, QuicPacketType.RETRY):
-            # not packet-protected: handed back for the connection's own handlers
+        if ptype == QuicPacketType.VERSION_NEGOTIATION:
+            # not packet-protected: handed back for the connection's own handler
+            out.append(ReceivedPacket(d, start, header, ptype, None))
+            return
+        # a long header of a version the configuration does not accept ends
+        # the datagram (connection.py:855-869)
+        if header.version is not None and header.version not in conn.supported_versions:
+            out.append(ReceivedPacket(d, start, header, ptype, None, dropped="unsupported_version"))
+            return
+        if ptype == QuicPacketType.RETRY:
             out.append(ReceivedPacket(d, start, header, ptype, None))
             return
         epoch = _EPOCH_OF_TYPE[ptype]

@@ -15,6 +15,12 @@ unprotect batch.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config ns] [--e2e]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+--gpus N without a launcher (WORLD_SIZE unset) starts N rank processes
+itself, one per visible GPU, before anything touches a GPU; with fewer than N
+visible GPUs it refuses unless --rehearse is given (ranks then share devices
+round-robin, a rehearsal of the launch path, not a scaling number).  Under a
+launcher WORLD_SIZE must equal N.
 """
 
 import argparse
@@ -81,7 +87,11 @@ def parse():
     ap.add_argument("--e2e-mode", choices=("staged", "per-chunk"), default="staged",
                     help="staged: one H2D, one compute and one D2H stream chained by events; "
                          "per-chunk: each chunk's copy/kernels/copy on one of --e2e-streams streams")
-    ap.add_argument("--check", action="store_true", help="verify round trip after timing")
+    ap.add_argument("--no-check", dest="check", action="store_false",
+                    help="skip the round-trip comparison after timing (default: every byte compared)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="allow more ranks than visible GPUs (devices shared round-robin)")
+    ap.add_argument("--master-port", type=int, default=0, help="rendezvous port of self-launched ranks")
     return ap.parse_args()
 
 
@@ -312,9 +322,61 @@ def key_schedule(eng_cls, n_keys, suite, version):
                     "host = HKDF only, 1 thread"}
 
 
+METRIC = "GiB/s device-resident AEAD protect+unprotect, 1200B packets, 1/2/4/8 MI355X"
+
+
+def plan_ranks(gpus: int, env: dict, visible: int, rehearse: bool):
+    """How this invocation runs: ("run", None) -- this process is one rank
+    (launched by torch.distributed.run, or N = 1); ("spawn", n) -- start n
+    rank processes; ("refuse", reason)."""
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: need at least one GPU"
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            return "refuse", f"WORLD_SIZE={world} but --gpus {gpus}: the launcher and the flag disagree"
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    if visible < gpus and not rehearse:
+        return "refuse", (f"--gpus {gpus} but {visible} GPU(s) visible; "
+                          "pass --rehearse to share devices (not a scaling number)")
+    return "spawn", gpus
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, port: int) -> int:
+    """Start ranks 0..n-1 of this command as child processes (this process
+    has not touched a GPU) and wait for them; returns the worst exit code."""
+    import subprocess
+
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
 def main():
     args = parse()
     import torch
+
+    # device_count() does not initialise the GPU on this image: safe before a spawn
+    mode, what = plan_ranks(args.gpus, os.environ, torch.cuda.device_count(), args.rehearse)
+    if mode == "refuse":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(what, args.master_port or _free_port()))
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -406,6 +468,7 @@ def main():
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize(dev)
+    elapsed_own = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -421,12 +484,21 @@ def main():
     hev_flags = hev.flags
     hev.close()
 
-    # every packet of the last step must authenticate (cheap, after timing)
+    # after timing: every packet of the last step authenticated, and (unless
+    # --no-check) the unprotected bytes equal the plaintext, every byte
     r1 = d_r1.cpu().numpy().view(L.RESULT)
     r2 = d_r2.cpu().numpy().view(L.RESULT)
-    ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all())
-    if args.check:
-        ok = ok and bool(torch.equal(d_back.cpu(), d_plain.cpu()))
+    tags_ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all())
+    rt_ok = bool(torch.equal(d_back, d_plain)) if args.check else None
+    ok = tags_ok and rt_ok is not False
+    mine = {"rank": rank, "device": local, "packets": n, "status_ok": ok, "tags_ok": tags_ok,
+            "round_trip_ok": rt_ok, "seconds": round(float(elapsed_own), 6),
+            "kernels_ms": {"protect": round(t_prot * 1e3, 4), "unprotect": round(t_unp * 1e3, 4)}}
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    ok = all(r["status_ok"] for r in per_rank)
 
     total_bytes = float(n) * 1200 * args.steps * world
     value = total_bytes / elapsed / GIB
@@ -446,7 +518,7 @@ def main():
     out = None
     if rank == 0:
         out = {
-            "metric": "GiB/s device-resident AEAD protect+unprotect, 1200B packets",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -479,6 +551,10 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "status_ok": ok,
+            "round_trip_checked": bool(args.check),
+            "ranks": per_rank,
+            "devices_visible": torch.cuda.device_count(),
+            "rehearsal_shared_devices": world > torch.cuda.device_count(),
         }
         if w.n_keys >= 64:
             out["key_schedule"] = key_schedule(PacketEngine, w.n_keys, cfg["suite"], cfg["version"])

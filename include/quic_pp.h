@@ -167,8 +167,9 @@ int qpp_unprotect(const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
  * connections (src/aioquic/asyncio/server.py:60-152 demultiplexes them per
  * datagram), but a kernel wants each workgroup on one key and one suite.
  * qpp_plan_build sorts the batch's packet indices on the device by
- * (suite, slot), stable within a bucket, and counts the packets of each
- * suite.  A *_planned launch gathers its descriptors into that order, runs
+ * (suite, slot) and counts the packets of each suite; the order of the
+ * packets within one (suite, slot) run is unspecified (results are mapped
+ * back to the caller's order, so it is not observable).  A *_planned launch gathers its descriptors into that order, runs
  * each suite's kernel over its own bucket only, and writes every result at
  * the packet's position in the CALLER's descriptor order.  A plan is built
  * once per batch and serves every launch over descriptors with the same

@@ -282,10 +282,13 @@ def test_aead_only_batch(oracle, L, engine_cls):
         assert np.array_equal(u[o : o + ln], uo[o : o + ln]), i
 
 
-@pytest.mark.parametrize("suite,version", [(0, 1), (2, 0x6B3343CF)], ids=["config2-aes128", "config3-chacha-v2"])
-def test_full_size_round_trip_64k(L, engine_cls, suite, version):
+@pytest.mark.parametrize("suite,version,n", [(0, 1, 1 << 16), (2, 0x6B3343CF, 1 << 16), (0, 1, 1 << 20)],
+                         ids=["config2-aes128", "config3-chacha-v2", "north-star-aes128-1Mi"])
+def test_full_size_round_trip(L, engine_cls, suite, version, n):
     """BASELINE configs 2 and 3 on device tensors: 64Ki x 1200 B, one key,
-    AES-128-GCM (QUIC v1) or ChaCha20-Poly1305 (QUIC v2 labels).
+    AES-128-GCM (QUIC v1) or ChaCha20-Poly1305 (QUIC v2 labels); and the
+    north-star shape itself, AES-128-GCM 1Mi x 1200 B with one key (the
+    1200-byte datagram of tests/test_packet_builder.py:490-522).
     Size-independent properties: round trip identity, all tags verify, every
     ciphertext differs from its plaintext, and the protected bytes against the
     oracle on a sampled subset."""
@@ -293,7 +296,6 @@ def test_full_size_round_trip_64k(L, engine_cls, suite, version):
 
     from aioquic_amd import bench_data
 
-    n = 65536
     w = bench_data.make_workload(n, suite=suite, n_keys=1, seed=0x9002, version=version)
     eng = engine_cls(w.n_keys)
     eng.set_key_records(w.keys)

@@ -285,3 +285,74 @@ def test_flush_builders_matches_oracle(oracle):
         assert [len(d) for d in dgrams] == [len(d) for d in want]
         assert dgrams == want
         assert [p.sent_bytes for p in packets] == [p.sent_bytes for p in tpackets]
+
+
+@pytest.mark.gpu
+def test_flush_builders_two_threads(oracle):
+    """Two threads flushing builders at once on the default key tables (one
+    per thread): every datagram still equals the oracle's."""
+    import threading
+
+    results, errors = {}, []
+
+    def work(tag):
+        try:
+            for rep in range(3):
+                builders, _ = _gpu_case(oracle, n_conn=4, per_conn=30)
+                twins, _ = _gpu_case(oracle, n_conn=4, per_conn=30)
+                got = PB.flush_builders(builders)
+                for (dgrams, _), twin in zip(got, twins):
+                    plains, pending, _ = twin._close()
+                    if dgrams != _oracle_protect(oracle)(plains, pending, None):
+                        errors.append((tag, rep))
+            results[tag] = True
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((tag, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errors, errors
+    assert results == {0: True, 1: True}
+
+
+@pytest.mark.gpu
+def test_key_slots_release_on_teardown_and_update():
+    """CryptoContext.teardown and a key update release the keys a batch table
+    holds: the slots are freed, reused, and the table's device
+    entries of released slots are cleared (a packet aimed at one reports
+    KeyUnavailable), while live keys keep working."""
+    from aioquic_amd._crypto import unprotect_host
+    from aioquic_amd.batch_io import KeySlots, SendBatch
+    from aioquic_amd.crypto import CryptoPair
+
+    def pair(cid):
+        p = CryptoPair()
+        p.setup_initial(cid, is_client=True, version=QuicProtocolVersion.VERSION_1)
+        return p
+
+    slots = KeySlots(8)
+    a, b = pair(bytes(8)), pair(bytes([1]) * 8)
+    sb = SendBatch(slots)
+    hdr = bytes([0x41]) + bytes(8) + bytes(2)
+    sb.add(a, hdr, bytes(40), 0)
+    sb.add(b, hdr, bytes(40), 0)
+    sb.flush()
+    assert len(slots._keep) == 2
+    a_slot = slots._slot[(id(a.send.aead), id(a.send.hp), 0)]
+    a.teardown()
+    assert len(slots._keep) == 1 and slots._free == [a_slot]
+    # the cleared device entry: unprotect aimed at it finds no key
+    desc = np.zeros(1, dtype=L.DESC)
+    desc["len"], desc["hdr_len"], desc["slot"] = 40, 9, a_slot
+    _, res = unprotect_host(slots.table, desc.tobytes(), bytes(40), 40)
+    assert np.frombuffer(res, dtype=L.RESULT)[0]["status"] == L.S_NO_KEY
+    # a key update releases the old AEAD; the new one reuses the freed slot
+    old = b.send.aead
+    b.update_key()
+    sb.add(b, bytes([0x45]) + bytes(8) + bytes(2), bytes(40), 1)
+    w = sb.flush()
+    assert len(w) == 1 and not any(k[0] == id(old) for k in slots._slot)
+    assert len(slots._keep) == 1

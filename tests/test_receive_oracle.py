@@ -1,0 +1,277 @@
+"""Batched receive (f2) against the oracle, not against itself.
+
+* CPU: the oracle's receive walk (oracle/receive_walk.py) is pinned by the
+  reference's own golden vectors, and the product's header parser agrees with
+  the oracle's on every datagram of the scenario.
+* GPU: receive_datagrams and ReceiveBatch run oracle-built traffic
+  (tests/receive_scenario.py) and the golden vectors' wire bytes; every
+  outcome -- drop trigger, plain header, payload, packet number -- and the
+  final expected packet numbers and key phases equal the oracle walk of
+  quic/connection.py:793-947.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import receive_walk as W
+from tests.golden_util import case_inputs, load_cases, matches, tamper
+from tests import receive_scenario as RS
+
+
+def _golden_wire(c, oracle):
+    """The golden case's protected packet (sender phase per the case),
+    checked against the reference's fixture, then tampered as the case says."""
+    x = case_inputs(c, oracle)
+    key, iv = (x["next_key"], x["next_iv"]) if c["send_phase"] else (x["key"], x["iv"])
+    wire = oracle.protect(c["suite"], key, iv, x["hp"], x["header"], x["payload"], c["pn"])
+    assert matches(c["protected"], wire), c["seed"]
+    return x, tamper(c, wire)
+
+
+def _walkable(c):
+    """Golden cases the receive walk decrypts: short headers, and v1 long
+    headers (type bits 00 = Initial; under v2 they read as Retry)."""
+    first = bytes.fromhex(c["header"])[0]
+    return not first & 0x80 or c["version"] == 1
+
+
+def _golden_items(oracle):
+    from oracle import oracle as O
+
+    out = []
+    for c in load_cases():
+        if not _walkable(c):
+            continue
+        x, wire = _golden_wire(c, oracle)
+        hdr = x["header"]
+        long = bool(hdr[0] & 0x80)
+        cid_len = 0 if long else c["pn_off"] - 1
+        # the walk must find this packet as one whole packet at the case's
+        # packet-number offset (a few long-header cases carry a Length field
+        # from before their payload was trimmed to the 1500-byte domain)
+        try:
+            h = W.parse_header(wire, 0, cid_len)
+        except W.ParseError:
+            continue
+        if h.packet_length != len(wire) or h.encrypted_offset != c["pn_off"]:
+            continue
+        conn = W.Conn(pairs={e: W.Pair(W.Ctx(c["suite"], x["secret"], c["version"]))
+                             for e in ("INITIAL", "HANDSHAKE", "ZERO_RTT", "ONE_RTT")},
+                      host_cid_length=cid_len, is_client=True,
+                      supported_versions=[O.VERSION_1, O.VERSION_2])
+        conn.expected = {k: c["expected_pn"] for k in ("INITIAL", "HANDSHAKE", "ONE_RTT")}
+        out.append((c, x, conn, wire))
+    return out
+
+
+def test_oracle_walk_matches_reference_golden(oracle):
+    """The oracle walk reproduces the reference's outcome for every golden
+    packet it can walk (plain header, payload, pn, failures)."""
+    n = 0
+    for c, x, conn, wire in _golden_items(oracle):
+        (o,) = W.receive([(conn, wire)])
+        exp = c["unprotect"]
+        if not exp["ok"]:
+            assert o.dropped == "payload_decrypt_error", c["seed"]
+            continue
+        assert o.dropped is None, c["seed"]
+        assert o.plain_header.hex() == exp["header"], c["seed"]
+        assert matches(exp["payload"], o.plain_payload), c["seed"]
+        assert o.packet_number == exp["pn"], c["seed"]
+        n += 1
+    assert n > 60
+
+
+def test_header_parse_matches_oracle():
+    """aioquic_amd.packet.pull_quic_header against the oracle's restatement of
+    packet.py:181-267 on every packet start of the scenario."""
+    from aioquic_amd.buffer import Buffer
+    from aioquic_amd.packet import pull_quic_header
+
+    specs, items = RS.build(n_conns=4, per_conn=12)
+    checked = 0
+    for _, data in items:
+        pos = 0
+        while pos < len(data):
+            try:
+                h = W.parse_header(data, pos, 8)
+            except W.ParseError:
+                with pytest.raises(ValueError):
+                    b = Buffer(data=data)
+                    b.seek(pos)
+                    pull_quic_header(b, host_cid_length=8)
+                break
+            b = Buffer(data=data)
+            b.seek(pos)
+            p = pull_quic_header(b, host_cid_length=8)
+            assert (p.version, p.packet_type.name, p.packet_length) == (h.version, h.packet_type, h.packet_length)
+            checked += 1
+            if h.packet_type in ("VERSION_NEGOTIATION", "RETRY"):
+                break  # not protected: no packet-number offset
+            assert b.tell() - pos == h.encrypted_offset
+            pos += h.packet_length
+    assert checked > 50
+
+
+def test_unsupported_version_dropped_cpu(monkeypatch, oracle):
+    """A grease-version long header ends the datagram as unsupported_version
+    (connection.py:855-869), before any decrypt."""
+    from aioquic_amd import receive as R
+
+    grease = RS.long_header(RS.GREASE_VERSION, "HANDSHAKE", bytes(8), bytes(8), b"", 0, 2, 40) + bytes(40)
+
+    class NoBatch:
+        def add(self, *a, **k):
+            raise AssertionError("nothing is decrypted")
+
+        def run(self):
+            return []
+
+    keys = R.ConnectionKeys(cryptos={}, spaces={}, is_client=True)
+    got = R.receive_datagrams([(keys, grease)], batch=NoBatch())
+    assert [(p.dropped, p.epoch) for p in got] == [("unsupported_version", None)]
+    (o,) = W.receive([(W.Conn(pairs={}, is_client=True), grease)])
+    assert o.dropped == "unsupported_version"
+
+
+def _product_tuple(p):
+    return (p.datagram, p.offset, p.packet_type.name, p.dropped, p.plain_header, p.plain_payload,
+            p.packet_number)
+
+
+def _oracle_tuple(o):
+    return (o.datagram, o.offset, o.packet_type, o.dropped, o.plain_header, o.plain_payload, o.packet_number)
+
+
+@pytest.mark.gpu
+def test_receive_datagrams_vs_oracle_walk():
+    from aioquic_amd.receive import receive_datagrams
+    from aioquic_amd.tls import Epoch
+
+    specs, items = RS.build()
+    oconns = [s.oracle_conn() for s in specs]
+    pconns = [s.product_conn() for s in specs]
+    want = W.receive([(oconns[c], d) for c, d in items])
+    got = receive_datagrams([(pconns[c], d) for c, d in items])
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert _product_tuple(g) == _oracle_tuple(w)
+    kinds = {w.dropped for w in want}
+    assert {None, "payload_decrypt_error", "key_unavailable", "unsupported_version", "header_parse_error",
+            "initial_packet_datagram_too_small"} <= kinds
+    # state after the batch: expected packet numbers and the rolled 1-RTT keys
+    for oc, pc in zip(oconns, pconns):
+        assert oc.expected["ONE_RTT"] == pc.spaces[Epoch.ONE_RTT].expected_packet_number
+        assert oc.expected["HANDSHAKE"] == pc.spaces[Epoch.HANDSHAKE].expected_packet_number
+        assert oc.expected["INITIAL"] == pc.spaces[Epoch.INITIAL].expected_packet_number
+        if oc.pairs["ONE_RTT"].recv is not None:
+            assert oc.pairs["ONE_RTT"].recv.key_phase == pc.cryptos[Epoch.ONE_RTT].recv.key_phase == 1
+
+
+@pytest.mark.gpu
+def test_receive_datagrams_golden_wire(oracle):
+    """The golden vectors' wire bytes through receive_datagrams: each outcome
+    equals the reference's recorded one."""
+    from aioquic_amd.crypto import CryptoPair
+    from aioquic_amd.receive import ConnectionKeys, receive_datagrams
+    from aioquic_amd.tls import CipherSuite, Epoch
+
+    cs = {0: CipherSuite.AES_128_GCM_SHA256, 1: CipherSuite.AES_256_GCM_SHA384,
+          2: CipherSuite.CHACHA20_POLY1305_SHA256}
+    gi = _golden_items(oracle)
+    items, cases = [], []
+    for c, x, conn, wire in gi:
+        pair = CryptoPair()
+        pair.recv.setup(cipher_suite=cs[c["suite"]], secret=x["secret"], version=c["version"])
+
+        class Space:
+            expected_packet_number = c["expected_pn"]
+
+        keys = ConnectionKeys(cryptos={e: pair for e in Epoch},
+                              spaces={e: Space() for e in (Epoch.INITIAL, Epoch.HANDSHAKE, Epoch.ONE_RTT)},
+                              cryptos_initial={c["version"]: pair}, host_cid_length=conn.host_cid_length,
+                              is_client=True)
+        items.append((keys, wire))
+        cases.append(c)
+    got = receive_datagrams(items)
+    assert len(got) == len(items)
+    for p, c in zip(got, cases):
+        exp = c["unprotect"]
+        if not exp["ok"]:
+            assert p.dropped == "payload_decrypt_error", c["seed"]
+            continue
+        assert p.dropped is None, c["seed"]
+        assert p.plain_header.hex() == exp["header"], c["seed"]
+        assert matches(exp["payload"], p.plain_payload), c["seed"]
+        assert p.packet_number == exp["pn"], c["seed"]
+
+
+@pytest.mark.gpu
+def test_receive_batch_vs_oracle_pairs():
+    """ReceiveBatch directly (one connection's 1-RTT stream with a key
+    update, tampering and reordering, expected numbers tracked by a space)
+    against the oracle's CryptoPair.decrypt_packet one packet at a time."""
+    from aioquic_amd.batch_io import ReceiveBatch
+    from aioquic_amd.tls import Epoch
+
+    specs, items = RS.build(n_conns=4, per_conn=120)
+    for ci in (1, 2):
+        spec = specs[ci]
+        stream = [d for c, d in items if c == ci][1:-2]  # the 1-RTT datagrams
+        oc, pc = spec.oracle_conn(), spec.product_conn()
+        batch = ReceiveBatch(capacity=8)
+        for d in stream:
+            batch.add(pc.cryptos[Epoch.ONE_RTT], d, 9, space=pc.spaces[Epoch.ONE_RTT])
+        got = batch.run()
+        opair = oc.pairs["ONE_RTT"]
+        for d, g in zip(stream, got):
+            try:
+                h, p, pn = opair.decrypt_packet(d, 9, oc.expected["ONE_RTT"])
+                if pn > oc.expected["ONE_RTT"]:
+                    oc.expected["ONE_RTT"] = pn + 1
+                assert g == (h, p, pn)
+            except (W.DecryptError, W.KeyUnavailable):
+                assert not isinstance(g, tuple)
+        assert oc.expected["ONE_RTT"] == pc.spaces[Epoch.ONE_RTT].expected_packet_number
+        # one launch per round: the first, the key roll, and no more for the
+        # corrupt and old-phase packets
+        assert batch.launches <= 4
+
+
+@pytest.mark.gpu
+def test_receive_batch_corrupt_packets_bounded_launches():
+    """Forged packets interleaved with good ones after the expected number has
+    moved cost no extra launch each (batch_io.py): 200 packets with
+    every 5th corrupted run in a bounded number of launches, with the same
+    outcomes as the oracle."""
+    from aioquic_amd.batch_io import ReceiveBatch
+    from aioquic_amd.tls import Epoch
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(99)
+    spec = RS.ConnSpec(rng, 1, O.VERSION_1, O.AES_128_GCM)
+    one = W.Ctx(spec.suite, spec.one_secret, spec.version)
+    pkts = []
+    for pn in range(200):
+        w = RS._protect(one, RS.short_header(spec.cid, 0, pn, 2), rng.bytes(100), pn)
+        if pn % 5 == 3:
+            b = bytearray(w)
+            b[20] ^= 1
+            w = bytes(b)
+        pkts.append(w)
+    oc, pc = spec.oracle_conn(), spec.product_conn()
+    batch = ReceiveBatch(capacity=4)
+    for w in pkts:
+        batch.add(pc.cryptos[Epoch.ONE_RTT], w, 9, space=pc.spaces[Epoch.ONE_RTT])
+    got = batch.run()
+    for w, g in zip(pkts, got):
+        try:
+            exp = oc.pairs["ONE_RTT"].decrypt_packet(w, 9, oc.expected["ONE_RTT"])
+            oc.expected["ONE_RTT"] = max(oc.expected["ONE_RTT"], exp[2] + 1)
+            assert g == exp
+        except W.DecryptError:
+            assert not isinstance(g, tuple)
+    assert sum(isinstance(g, tuple) for g in got) == 160
+    assert batch.launches <= 2, batch.launches

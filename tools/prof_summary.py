@@ -13,19 +13,82 @@ exact for 16 B/lane stores.  Both corrections are stated next to the numbers.
 import collections
 import csv
 import glob
+import json
 import os
 import sys
+
+BYTES_PER_PKT_KERNEL = 2440  # bench.py: algorithmic HBM bytes per packet per launch
+HBM_PEAK_GBS = 8000.0
 
 
 def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
-def main(d):
+def bench_line(d):
+    """The bench's JSON line from the kernel-trace pass's log."""
+    try:
+        for line in open(os.path.join(d, "kt.log")):
+            if line.startswith("{") and '"metric"' in line:
+                return json.loads(line)
+    except OSError:
+        pass
+    return None
+
+
+def timed_launches(d, out_csv=None):
+    """Per kernel, the dispatches of the bench's K timed steps only (the
+    first W steps are warm-up at a lower clock): each step launches every
+    kernel the same number of times, so the timed ones are the last
+    K x (calls / (W + K)) dispatches of each kernel in dispatch order."""
+    b = bench_line(d)
+    traces = glob.glob(os.path.join(d, "kt", "*kernel_trace.csv"))
+    if not b or not traces:
+        return None, b
+    rows = list(csv.DictReader(open(traces[0])))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    by = collections.defaultdict(list)
+    for r in rows:
+        by[short(r["Kernel_Name"])].append(r)
+    steps, warm = int(b["steps"]), int(b["warmup"])
+    keep = {}
+    for k, rs in by.items():
+        if len(rs) % (steps + warm):
+            continue  # not a per-step kernel (setup, copies, the HBM copy probe)
+        per = len(rs) // (steps + warm)
+        keep[k] = rs[len(rs) - steps * per:]
+    if out_csv:
+        kept = sorted((r for rs in keep.values() for r in rs), key=lambda r: int(r["Start_Timestamp"]))
+        with open(out_csv, "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+            w.writeheader()
+            w.writerows(kept)
+    return keep, b
+
+
+def main(d, timed_csv=None):
+    keep, b = timed_launches(d, timed_csv)
+    if keep:
+        n = int(b["config"]["packets_per_gpu"])
+        print(f"# rocprofv3 summary: `{os.path.basename(d.rstrip('/'))}`\n")
+        print(f"## Timed launches only ({b['steps']} timed steps after {b['warmup']} warm-up steps; "
+              f"`{b['config']['workload']}`)\n")
+        print("| kernel | timed calls | avg us | min us | max us | algorithmic GB/s | frac of 8 TB/s |")
+        print("|---|---:|---:|---:|---:|---:|---:|")
+        for k, rs in sorted(keep.items(), key=lambda kv: -sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                                                               for r in kv[1])):
+            ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rs]
+            avg = sum(ds) / len(ds)
+            gbs = BYTES_PER_PKT_KERNEL * n / (avg * 1e-6) / 1e9 if ("k_gcm" in k or "k_chacha" in k) else None
+            extra = f"{gbs:.1f} | {gbs / HBM_PEAK_GBS:.4f}" if gbs else "- | -"
+            print(f"| `{k}` | {len(ds)} | {avg:.2f} | {min(ds):.2f} | {max(ds):.2f} | {extra} |")
+        print(f"\nThe bench line of this run: value {b['value']} {b['unit']}, kernels_ms {b['kernels_ms']}, "
+              f"roofline.frac {b['roofline']['frac']}.\n")
     stats = os.path.join(d, "kt", "kt_kernel_stats.csv")
     rows = list(csv.DictReader(open(stats)))
-    print(f"# rocprofv3 summary: `{os.path.basename(d.rstrip('/'))}`\n")
-    print("## Kernel trace (`rocprofv3 --kernel-trace --stats`)\n")
+    if not keep:
+        print(f"# rocprofv3 summary: `{os.path.basename(d.rstrip('/'))}`\n")
+    print("## Kernel trace, every launch (`rocprofv3 --kernel-trace --stats`)\n")
     print("| kernel | calls | avg us | min us | max us | % time |")
     print("|---|---:|---:|---:|---:|---:|")
     for r in rows:
@@ -69,4 +132,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
