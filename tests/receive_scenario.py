@@ -78,9 +78,12 @@ class ConnSpec:
               O.CHACHA20_POLY1305: CipherSuite.CHACHA20_POLY1305_SHA256}
 
         def pair(suite, secret):
+            # both directions keyed, as a connection's pairs are: a peer key
+            # update rolls send and recv together (crypto.py:243-246)
             p = CryptoPair()
             if secret is not None:
                 p.recv.setup(cipher_suite=cs[suite], secret=secret, version=self.version)
+                p.send.setup(cipher_suite=cs[suite], secret=secret[::-1], version=self.version)
             return p
 
         init = CryptoPair()

@@ -16,7 +16,7 @@ fi
 for c in "${CFGS[@]}"; do
   for v in base "$@"; do
     if [ "$v" = base ]; then LP=""; else LP="$GRAFT_REPO_ROOT/variants/$v"; fi
-    LD_LIBRARY_PATH=$LP timeout -k 10 150 python -u bench.py --config $c --packets ${PKTS:-0} --check --steps ${STEPS:-20} --warmup 5 --cpu-seconds 0 --cpu-all-cores 0 > $O/b_${c}_$v.json 2> $O/b_${c}_$v.err || { echo "fail $c $v"; tail -5 $O/b_${c}_$v.err; exit 1; }
+    LD_LIBRARY_PATH=$LP timeout -k 10 150 python -u bench.py --config $c --packets ${PKTS:-0} --steps ${STEPS:-20} --warmup 5 --cpu-seconds 0 --cpu-all-cores 0 > $O/b_${c}_$v.json 2> $O/b_${c}_$v.err || { echo "fail $c $v"; tail -5 $O/b_${c}_$v.err; exit 1; }
     python3 -c "import json; d=json.loads(open('$O/b_${c}_$v.json').read().strip().split(chr(10))[-1]); print('$c $v', d['value'], d['kernels_ms'], d.get('check'), d['status_ok'])"
   done
 done

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing-only A/B (no --check: ablation variants compute wrong bytes) of the
+# Timing-only A/B (no: ablation variants compute wrong bytes) of the
 # in-tree library against variants/<name>/ builds: tools/gpu_abl.sh cfg packets variant...
 set -uo pipefail
 CFG=$1; PK=$2; shift 2

@@ -13,7 +13,7 @@ fi
 for cfg in ${CFGS:-ns 4}; do
   for v in ${VARS:-1:1024 2:1024 2:768 1:1024 2:1024}; do
     b=${v%%:*}; w=${v#*:}
-    QPP_GCM_BPL=$b QPP_WG_GCM=$w timeout -k 10 150 python -u bench.py --config $cfg --check --steps 20 --warmup 5 --cpu-seconds 0 > $O/b_${cfg}_${b}_${w}.json 2> $O/b.err || { echo "fail $cfg $v"; tail -3 $O/b.err; exit 1; }
+    QPP_GCM_BPL=$b QPP_WG_GCM=$w timeout -k 10 150 python -u bench.py --config $cfg --steps 20 --warmup 5 --cpu-seconds 0 > $O/b_${cfg}_${b}_${w}.json 2> $O/b.err || { echo "fail $cfg $v"; tail -3 $O/b.err; exit 1; }
     python3 -c "import json; d=json.loads(open('$O/b_${cfg}_${b}_${w}.json').read().strip().split(chr(10))[-1]); print('$cfg bpl=$b wg=$w', d['value'], d['kernels_ms'], d.get('check'))"
   done
 done

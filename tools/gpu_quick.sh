@@ -11,6 +11,6 @@ if [ -z "$NOTEST" ]; then
 fi
 for a in "$@"; do
   c=${a%%:*}; o=${a#*:}
-  timeout -k 10 200 python -u bench.py --config $c --order $o ${LAYOUT:+--layout $LAYOUT} --check --steps 10 --warmup 3 --cpu-seconds 0 > $O/b_${c}_$o.json 2> $O/b.err || { echo "fail $a"; tail -3 $O/b.err; exit 1; }
+  timeout -k 10 200 python -u bench.py --config $c --order $o ${LAYOUT:+--layout $LAYOUT} --steps 10 --warmup 3 --cpu-seconds 0 > $O/b_${c}_$o.json 2> $O/b.err || { echo "fail $a"; tail -3 $O/b.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$O/b_${c}_$o.json').read().strip().split(chr(10))[-1]); print('$a', d['value'], d['kernels_ms'], d.get('check'))"
 done
