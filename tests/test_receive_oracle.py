@@ -185,6 +185,7 @@ def test_receive_datagrams_golden_wire(oracle):
     for c, x, conn, wire in gi:
         pair = CryptoPair()
         pair.recv.setup(cipher_suite=cs[c["suite"]], secret=x["secret"], version=c["version"])
+        pair.send.setup(cipher_suite=cs[c["suite"]], secret=x["secret"][::-1], version=c["version"])
 
         class Space:
             expected_packet_number = c["expected_pn"]
