@@ -306,8 +306,66 @@ class ReceiveBatch:
         r = np.frombuffer(res, dtype=L.RESULT)
         return outs, r["status"].tolist(), r["pn"].tolist(), r["hdr_len"].tolist()
 
-    def run(self) -> list:
+    def _walk(self, todo, speculate, r_out, r_st, r_pn, r_hl, exp_at, rolled_at):
+        """One round's in-order walk over the launch results, with every state
+        change deferred: returns (outcomes by item, stale items, speculated
+        items [(item, expected number)], pairs to roll, {space: (space, new
+        expected number)}).  Keys change only at a roll, which blocks its pair
+        for the rest of the round, so every unblocked pair still has its
+        launch-time keys.
+
+        A packet decoded under an expected number an earlier packet has since
+        raised needs another launch only if its number (hence nonce) decodes
+        differently now.  A failed tag check reports its number too; length
+        and missing-key failures do not depend on the expected number.  With
+        `speculate`, such a failed packet is taken to fail again (a corrupt
+        or forged packet does, whatever its number) and listed for one
+        confirming launch instead of blocking its pair."""
         pairs, spaces, track, offs = self._pairs, self._spaces, self._track, self._offs
+        got: dict = {}
+        stale, spec, rolls = [], [], []
+        blocked: set = set()
+        exp: dict = {}
+        for i in todo:
+            pair = pairs[i]
+            if blocked and id(pair) in blocked:
+                stale.append(i)
+                continue
+            if pair.recv.aead is None:
+                got[i] = KeyUnavailableError("Decryption key is not available")
+                continue
+            status = r_st[i]
+            if status is None:  # the offset check failed
+                got[i] = CryptoError("Invalid payload length")
+                continue
+            space = spaces[i]
+            held = exp.get(id(space))
+            exp_now = held[1] if held else space.expected_packet_number
+            pn = r_pn[i]
+            if exp_now != exp_at[i] and status in (L.S_OK, L.S_DECRYPT):
+                pn_len = r_hl[i] - offs[i]
+                if decode_packet_number(_signed_trunc(pn, pn_len), pn_len * 8, exp_now) != pn:
+                    if speculate and status == L.S_DECRYPT and i not in rolled_at:
+                        spec.append((i, exp_now))
+                        got[i] = _raise_status(status)
+                        continue
+                    blocked.add(id(pair))
+                    stale.append(i)
+                    continue
+            if status != L.S_OK:
+                got[i] = _raise_status(status)
+                continue
+            out = r_out[i]
+            got[i] = (out[0], out[1], pn)
+            if i in rolled_at:
+                rolls.append(pair)
+                blocked.add(id(pair))
+            if track[i] and pn > exp_now:
+                exp[id(space)] = (space, pn + 1)
+        return got, stale, spec, rolls, exp
+
+    def run(self) -> list:
+        pairs, spaces, offs = self._pairs, self._spaces, self._offs
         n = len(pairs)
         outcome: list = [None] * n
         todo = list(range(n))
@@ -350,48 +408,30 @@ class ReceiveBatch:
                 for k, i in enumerate(idx):
                     r_out[i], r_st[i], r_pn[i], r_hl[i] = outs[k], st[k], pn[k], hl[k]
                     rolled_at.add(i)
-            # walk in order, applying each packet's effect on its pair.  Keys
-            # only change here (a roll blocks its pair for the rest of the
-            # round), so every unblocked pair still has its launch-time keys.
-            blocked: set = set()
-            stale = []
-            for i in todo:
-                pair = pairs[i]
-                if blocked and id(pair) in blocked:
-                    stale.append(i)
-                    continue
-                if pair.recv.aead is None:
-                    outcome[i] = KeyUnavailableError("Decryption key is not available")
-                    continue
-                status = r_st[i]
-                if status is None:  # the offset check failed
-                    outcome[i] = CryptoError("Invalid payload length")
-                    continue
-                space = spaces[i]
-                exp_now = space.expected_packet_number
-                moved = exp_now != exp_at[i]
-                pn = r_pn[i]
-                # decoded under an expected number an earlier packet has since
-                # raised: only a packet whose number (hence nonce) decodes
-                # differently now needs another launch.  A failed tag check
-                # reports its number too; length and missing-key failures do
-                # not depend on the expected number at all.
-                if moved and status in (L.S_OK, L.S_DECRYPT):
-                    pn_len = r_hl[i] - offs[i]
-                    if decode_packet_number(_signed_trunc(pn, pn_len), pn_len * 8, exp_now) != pn:
-                        blocked.add(id(pair))
-                        stale.append(i)
-                        continue
-                if status != L.S_OK:
-                    outcome[i] = _raise_status(status)
-                    continue
-                out = r_out[i]
-                outcome[i] = (out[0], out[1], pn)
-                if i in rolled_at:
-                    pair._update_key("remote_update")
-                    blocked.add(id(pair))
-                if track[i] and pn > exp_now:
-                    space.expected_packet_number = pn + 1
+            # walk in order, applying each packet's effect on its pair
+            got, stale, spec, rolls, exp = self._walk(todo, True, r_out, r_st, r_pn, r_hl, exp_at, rolled_at)
+            if spec:
+                # failed packets whose number now decodes differently were
+                # assumed to fail again: check them all in one launch (their
+                # keys are the launch-time ones: no roll is applied yet)
+                idx = [i for i, _ in spec]
+                triples = [(pairs[i].recv.aead, pairs[i].recv.hp, pairs[i].recv.key_phase) for i in idx]
+                _, st, _, _ = self._launch(idx, triples, [e for _, e in spec])
+                if any(x == L.S_OK for x in st):
+                    # a packet the walk took for a failure authenticates now:
+                    # walk the round again without assuming (rare)
+                    got, stale, spec, rolls, exp = self._walk(todo, False, r_out, r_st, r_pn, r_hl, exp_at,
+                                                              rolled_at)
+                else:
+                    for i, x in zip(idx, st):
+                        got[i] = _raise_status(x)
+            # commit the round: outcomes, expected packet numbers, key rolls
+            for i, o in got.items():
+                outcome[i] = o
+            for space, v in exp.values():
+                space.expected_packet_number = v
+            for pair in rolls:
+                pair._update_key("remote_update")
             for i in stale:
                 r_st[i] = None
             todo = stale
