@@ -345,7 +345,7 @@ class ReceiveBatch:
             if exp_now != exp_at[i] and status in (L.S_OK, L.S_DECRYPT):
                 pn_len = r_hl[i] - offs[i]
                 if decode_packet_number(_signed_trunc(pn, pn_len), pn_len * 8, exp_now) != pn:
-                    if speculate and status == L.S_DECRYPT and i not in rolled_at:
+                    if speculate and status == L.S_DECRYPT:
                         spec.append((i, exp_now))
                         got[i] = _raise_status(status)
                         continue
@@ -380,9 +380,11 @@ class ReceiveBatch:
             # a pn offset beyond the header limit fails host-side (length)
             launch = [i for i in todo if pairs[i].recv.aead is not None and offs[i] <= L.MAX_HDR]
             keys = []
+            used: dict = {}  # item -> the (aead, hp, key_phase) it was decrypted with
             for i in launch:
                 rc = pairs[i].recv
                 keys.append((rc.aead, rc.hp, rc.key_phase))
+                used[i] = keys[-1]
                 exp_at[i] = spaces[i].expected_packet_number
             flip = []
             if launch:
@@ -408,15 +410,15 @@ class ReceiveBatch:
                 for k, i in enumerate(idx):
                     r_out[i], r_st[i], r_pn[i], r_hl[i] = outs[k], st[k], pn[k], hl[k]
                     rolled_at.add(i)
+                    used[i] = triples[k]
             # walk in order, applying each packet's effect on its pair
             got, stale, spec, rolls, exp = self._walk(todo, True, r_out, r_st, r_pn, r_hl, exp_at, rolled_at)
             if spec:
                 # failed packets whose number now decodes differently were
-                # assumed to fail again: check them all in one launch (their
-                # keys are the launch-time ones: no roll is applied yet)
+                # assumed to fail again: check them all in one launch, each
+                # with the keys it was tried with (no roll is applied yet)
                 idx = [i for i, _ in spec]
-                triples = [(pairs[i].recv.aead, pairs[i].recv.hp, pairs[i].recv.key_phase) for i in idx]
-                _, st, _, _ = self._launch(idx, triples, [e for _, e in spec])
+                _, st, _, _ = self._launch(idx, [used[i] for i in idx], [e for _, e in spec])
                 if any(x == L.S_OK for x in st):
                     # a packet the walk took for a failure authenticates now:
                     # walk the round again without assuming (rare)

@@ -275,4 +275,4 @@ def test_receive_batch_corrupt_packets_bounded_launches():
         except W.DecryptError:
             assert not isinstance(g, tuple)
     assert sum(isinstance(g, tuple) for g in got) == 160
-    assert batch.launches <= 2, batch.launches
+    assert batch.launches <= 3, batch.launches  # the batch, the key-phase retry, one check
