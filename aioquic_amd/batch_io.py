@@ -40,7 +40,7 @@ import numpy as np
 
 from . import crypto as crypto_mod
 from . import layout as L
-from ._crypto import CryptoError, KeyTable, protect_list, unprotect_list
+from ._crypto import CryptoError, KeyTable, protect_list, unprotect_list, unprotect_walk
 from .crypto import CryptoContext, CryptoPair, KeyUnavailableError, next_key_phase
 from .packet import decode_packet_number
 
@@ -291,6 +291,71 @@ class ReceiveBatch:
         self._track.append(track)
         return len(self._pairs) - 1
 
+    def _extend(self, pairs: list, packets: list, offs: list, spaces: list) -> None:
+        """add() for many packets at once, each with a tracked space (the
+        batched receive walk's form: packets are bytes, no copies)."""
+        self._pairs += pairs
+        self._packets += packets
+        self._offs += offs
+        self._spaces += spaces
+        self._track += [True] * len(pairs)
+
+    def _fast_round(self, outcome: list) -> list:
+        """The first round in C (_crypto.unprotect_walk): one launch and the
+        in-order walk for every packet whose outcome no state change of this
+        round can alter; returns the deferred items (in order) for the
+        general rounds of run()."""
+        pairs, spaces, offs, track = self._pairs, self._spaces, self._offs, self._track
+        n = len(pairs)
+        launch = [i for i in range(n) if pairs[i].recv.aead is not None and offs[i] <= L.MAX_HDR]
+        if len(launch) != n:
+            for i in set(range(n)).difference(launch):
+                outcome[i] = (KeyUnavailableError("Decryption key is not available") if pairs[i].recv.aead is None
+                              else CryptoError("Invalid payload length"))
+        if not launch:
+            return []
+        # pairs and spaces by identity, each resolved once
+        pix: dict = {}
+        six: dict = {}
+        p_of = [pix.setdefault(id(pairs[i]), len(pix)) for i in launch]
+        s_of = [six.setdefault(id(spaces[i]), len(six)) for i in launch]
+        upairs = [None] * len(pix)
+        for i, k in zip(launch, p_of):
+            upairs[k] = pairs[i]
+        uspaces = [None] * len(six)
+        for i, k in zip(launch, s_of):
+            uspaces[k] = spaces[i]
+        keys = _KeyRefs()
+        prefs = [keys.ref(p.recv.aead, p.recv.hp, p.recv.key_phase) for p in upairs]
+        pslot = np.asarray(self.slots.assign(keys.triples), dtype=np.uint32)[np.asarray(prefs, np.int64)]
+        p_arr = np.asarray(p_of, dtype=np.uint32)
+        s_arr = np.asarray(s_of, dtype=np.uint32)
+        sexp = np.asarray([sp.expected_packet_number & 0xFFFFFFFFFFFFFFFF for sp in uspaces], dtype=np.uint64)
+        outs, res, deferred, sexp2 = unprotect_walk(
+            self.slots.table, pslot[p_arr].tobytes(), sexp[s_arr].tobytes(),
+            [self._packets[i] for i in launch] if len(launch) != n else self._packets,
+            np.asarray([min(offs[i], 0xFFFF) for i in launch], np.uint32).tobytes(),
+            p_arr.tobytes(), s_arr.tobytes(), np.asarray([track[i] for i in launch], np.uint8).tobytes(),
+            sexp.tobytes(), len(upairs))
+        self.launches += 1
+        # outcomes: successes come as (header, payload, pn); failures by status
+        st = np.frombuffer(res, dtype=L.RESULT)["status"]
+        fail = np.flatnonzero(st != L.S_OK)
+        dset = set(deferred)
+        for k in fail.tolist():
+            if k not in dset:
+                outs[k] = _raise_status(int(st[k]))
+        if len(launch) == n:
+            outcome[:] = outs
+        else:
+            for k, i in enumerate(launch):
+                outcome[i] = outs[k]
+        # the spaces' expected numbers after the walk (only tracked spaces move)
+        new = np.frombuffer(sexp2, dtype=np.uint64)
+        for k in np.flatnonzero(new != sexp).tolist():
+            uspaces[k].expected_packet_number = int(new[k])
+        return [launch[k] for k in deferred]
+
     def _launch(self, idx: list, triples: list, expected: list):
         """One unprotect launch over items idx with per-item (aead, hp,
         key_phase); returns (list of (header, payload) | None, status list,
@@ -368,7 +433,8 @@ class ReceiveBatch:
         pairs, spaces, offs = self._pairs, self._spaces, self._offs
         n = len(pairs)
         outcome: list = [None] * n
-        todo = list(range(n))
+        # the first round in C; the general rounds below take what it defers
+        todo = self._fast_round(outcome)
         # per item of the current round, by item index
         r_out: list = [None] * n
         r_st: list = [None] * n

@@ -841,6 +841,269 @@ done:
 static PyObject *py_protect_list(PyObject *m, PyObject *args) { return batch_list(args, 1); }
 static PyObject *py_unprotect_list(PyObject *m, PyObject *args) { return batch_list(args, 0); }
 
+/* A per-packet array argument ("y#": any read-only bytes-like object)
+ * must hold exactly n items of `size` bytes. */
+static int check_len(Py_ssize_t len, Py_ssize_t n, Py_ssize_t size, const char *what)
+{
+    if (len == n * size) return 0;
+    PyErr_Format(PyExc_ValueError, "%s: %zd bytes for %zd items of %zd", what, len, n, size);
+    return -1;
+}
+
+/* protect_datagrams(table, plains, dg_u32, off_u32, hsize_u32, size_u32, pn_u64, slot_u32)
+ *     -> (wire datagrams, results)
+ * The deferred-encryption builder's flush (QuicPacketBuilder._end_packet,
+ * packet_builder.py:341-350, for every packet of every datagram at once):
+ * the plaintext datagrams go back to back into the session's pinned staging;
+ * packet k of datagram dg[k] starts at off[k] with hsize[k] header bytes and
+ * size[k] header + payload bytes (its tag's room follows).  Each wire
+ * datagram comes back as one bytes object cut from the pinned output, which
+ * the session writes in full (zeros outside packets: the builder's datagram
+ * padding is zeros too). */
+static PyObject *py_protect_datagrams(PyObject *m, PyObject *args)
+{
+    PyObject *t, *plains;
+    const char *a_dg, *a_off, *a_hs, *a_sz, *a_pn, *a_sl;
+    Py_ssize_t l_dg, l_off, l_hs, l_sz, l_pn, l_sl;
+    if (!PyArg_ParseTuple(args, "OO!y#y#y#y#y#y#", &t, &PyList_Type, &plains, &a_dg, &l_dg, &a_off, &l_off, &a_hs,
+                          &l_hs, &a_sz, &l_sz, &a_pn, &l_pn, &a_sl, &l_sl))
+        return NULL;
+    qpp_keytab *kt = as_table(t);
+    if (!kt) return NULL;
+    const Py_ssize_t nd = PyList_Size(plains), n = l_dg / 4;
+    if (check_len(l_dg, n, 4, "dg") < 0 || check_len(l_off, n, 4, "off") < 0 || check_len(l_hs, n, 4, "hsize") < 0 ||
+        check_len(l_sz, n, 4, "size") < 0 || check_len(l_pn, n, 8, "pn") < 0 || check_len(l_sl, n, 4, "slot") < 0)
+        return NULL;
+    PyObject *ret = NULL, *wires = NULL, *res = NULL;
+    size_t *base = NULL;
+    qpp_desc *desc = NULL;
+    base = (size_t *)malloc(((size_t)nd + 1) * sizeof(size_t));
+    desc = (qpp_desc *)calloc(n ? (size_t)n : 1, sizeof(qpp_desc));
+    res = PyBytes_FromStringAndSize(NULL, n * (Py_ssize_t)sizeof(qpp_result));
+    if (!base || !desc || !res) {
+        PyErr_NoMemory();
+        goto done;
+    }
+    base[0] = 0;
+    for (Py_ssize_t d = 0; d < nd; ++d) {
+        PyObject *o = PyList_GetItem(plains, d);
+        if (!PyBytes_Check(o)) {
+            PyErr_SetString(PyExc_TypeError, "datagrams must be bytes");
+            goto done;
+        }
+        base[d + 1] = base[d] + (size_t)PyBytes_Size(o);
+    }
+    {
+        const uint32_t *dg = (const uint32_t *)a_dg, *off = (const uint32_t *)a_off, *hs = (const uint32_t *)a_hs,
+                       *sz = (const uint32_t *)a_sz, *sl = (const uint32_t *)a_sl;
+        const uint64_t *pn = (const uint64_t *)a_pn;
+        for (Py_ssize_t k = 0; k < n; ++k) {
+            if (dg[k] >= (uint32_t)nd || hs[k] > sz[k] ||
+                (size_t)off[k] + sz[k] + QPP_TAG_LEN > base[dg[k] + 1] - base[dg[k]]) {
+                PyErr_SetString(PyExc_ValueError, "packet outside its datagram");
+                goto done;
+            }
+            qpp_desc *x = &desc[k];
+            x->in_off = x->out_off = base[dg[k]] + off[k];
+            x->hdr_len = hs[k] > 0xffff ? 0xffff : (uint16_t)hs[k];
+            x->len = sz[k] - hs[k];
+            x->pn = pn[k];
+            x->slot = sl[k];
+        }
+    }
+    {
+        const size_t total = base[nd];
+        qpp_session *s = session();
+        uint8_t *hin, *hout;
+        if (!s || check_rc(qpp_session_stage(s, total ? total : 1, (uint32_t)(n ? n : 1), &hin, &hout)) < 0)
+            goto done;
+        for (Py_ssize_t d = 0; d < nd; ++d)
+            memcpy(hin + base[d], PyBytes_AsString(PyList_GetItem(plains, d)), base[d + 1] - base[d]);
+        const uint8_t *src = hin;  /* no packet: the datagrams as they are */
+        if (n) {
+            if (host_call(1, kt, desc, (uint32_t)n, hin, total, hout, total, PyBytes_AsString(res)) < 0) goto done;
+            src = hout;
+        }
+        wires = PyList_New(nd);
+        if (!wires) goto done;
+        for (Py_ssize_t d = 0; d < nd; ++d) {
+            PyObject *o = PyBytes_FromStringAndSize((const char *)src + base[d], (Py_ssize_t)(base[d + 1] - base[d]));
+            if (!o) {
+                Py_CLEAR(wires);
+                goto done;
+            }
+            PyList_SetItem(wires, d, o);
+        }
+        ret = PyTuple_Pack(2, wires, res);
+    }
+done:
+    Py_XDECREF(wires);
+    Py_XDECREF(res);
+    free(base);
+    free(desc);
+    return ret;
+}
+
+/* decode_packet_number (quic/packet.py:118-132) of the truncated number as
+ * HeaderProtection.remove hands it over: a signed C int (_crypto.c:349), so a
+ * 4-byte value >= 2^31 enters negative, exactly as the Python walk sees it.
+ * Returns -1 where Python would produce a negative number. */
+static int64_t decode_pn_signed(uint64_t pn, int pn_len, uint64_t expected)
+{
+    const int bits = 8 * pn_len;
+    int64_t trunc = (int64_t)(pn & ((1ull << bits) - 1));
+    if (pn_len == 4 && trunc >= ((int64_t)1 << 31)) trunc -= (int64_t)1 << 32;
+    const int64_t window = (int64_t)1 << bits, half = window / 2, exp = (int64_t)expected;
+    const int64_t cand = (exp & ~(window - 1)) | trunc;
+    int64_t r;
+    if (cand <= exp - half && cand < ((int64_t)1 << 62) - window) r = cand + window;
+    else if (cand > exp + half && cand >= window) r = cand - window;
+    else r = cand;
+    return r < 0 ? -1 : r;
+}
+
+/* unprotect_walk(table, slots_u32, exp_u64, packets, offs_u32, pair_u32,
+ *                space_u32, track_u8, space_exp_u64, n_pairs)
+ *     -> (outcomes, results, deferred, space_exp_u64 after the walk)
+ * One ReceiveBatch round in C: the launch (as unprotect_list, each packet
+ * decoded against exp[i], its space's expected number when the round began)
+ * and the in-order walk of CryptoPair.decrypt_packet semantics
+ * (quic/crypto.py:184-192, connection.py:905-947,984-985) for every packet
+ * whose outcome does not depend on a state change this round makes:
+ *   outcomes[i] = (plain_header, payload, packet_number) on success, None on
+ *   failure (results[i].status says which), or None for a deferred packet;
+ *   the returned copy of space_exp advances as connection.py:984-985 does
+ *   (for track[i]).
+ * A packet is deferred -- and with it every later packet of its pair and of
+ * its space -- when its key phase flipped (a key roll follows), or when its
+ * truncated number decodes differently under the space's expected number by
+ * now than under exp[i].  The caller's general walk (batch_io.ReceiveBatch)
+ * then continues with the deferred packets, in order, from the state left
+ * here. */
+static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
+{
+    PyObject *t, *packets;
+    const char *a_sl, *a_exp, *a_offs, *a_pair, *a_space, *a_track, *a_sexp;
+    Py_ssize_t l_sl, l_exp, l_offs, l_pair, l_space, l_track, l_sexp;
+    unsigned int n_pairs;
+    if (!PyArg_ParseTuple(args, "Oy#y#O!y#y#y#y#y#I", &t, &a_sl, &l_sl, &a_exp, &l_exp, &PyList_Type, &packets,
+                          &a_offs, &l_offs, &a_pair, &l_pair, &a_space, &l_space, &a_track, &l_track, &a_sexp,
+                          &l_sexp, &n_pairs))
+        return NULL;
+    qpp_keytab *kt = as_table(t);
+    if (!kt) return NULL;
+    const Py_ssize_t n = PyList_Size(packets);
+    if (check_len(l_sl, n, 4, "slots") < 0 || check_len(l_exp, n, 8, "exp") < 0 ||
+        check_len(l_offs, n, 4, "offs") < 0 || check_len(l_pair, n, 4, "pair") < 0 ||
+        check_len(l_space, n, 4, "space") < 0 || check_len(l_track, n, 1, "track") < 0 || l_sexp % 8)
+        return l_sexp % 8 ? (PyErr_SetString(PyExc_ValueError, "space_exp: whole u64 items"), NULL) : NULL;
+    const Py_ssize_t n_spaces = l_sexp / 8;
+    const uint32_t *slots = (const uint32_t *)a_sl, *offs = (const uint32_t *)a_offs, *pair = (const uint32_t *)a_pair,
+                   *space = (const uint32_t *)a_space;
+    const uint64_t *exp = (const uint64_t *)a_exp;
+    const uint8_t *track = (const uint8_t *)a_track;
+    PyObject *ret = NULL, *outs = NULL, *res = NULL, *deferred = NULL, *sexp_out = NULL;
+    qpp_desc *desc = NULL;
+    uint8_t *blocked_pair = NULL, *blocked_space = NULL;
+    sexp_out = PyBytes_FromStringAndSize(a_sexp, l_sexp);  /* the spaces' expected numbers, advanced below */
+    if (!sexp_out) return NULL;
+    uint64_t *sx = (uint64_t *)PyBytes_AsString(sexp_out);
+    for (Py_ssize_t i = 0; i < n; ++i)
+        if (pair[i] >= n_pairs || (Py_ssize_t)space[i] >= n_spaces) {
+            PyErr_SetString(PyExc_ValueError, "pair or space index out of range");
+            goto done;
+        }
+    /* sizes, then the launch over the session's pinned staging */
+    size_t total = 0;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject *o = PyList_GetItem(packets, i);
+        if (!PyBytes_Check(o)) {
+            PyErr_SetString(PyExc_TypeError, "packets must be bytes");
+            goto done;
+        }
+        total += (size_t)PyBytes_Size(o);
+    }
+    desc = (qpp_desc *)calloc(n ? (size_t)n : 1, sizeof(qpp_desc));
+    res = PyBytes_FromStringAndSize(NULL, n * (Py_ssize_t)sizeof(qpp_result));
+    blocked_pair = (uint8_t *)calloc(n_pairs ? n_pairs : 1, 1);
+    blocked_space = (uint8_t *)calloc(n_spaces ? (size_t)n_spaces : 1, 1);
+    outs = PyList_New(n);
+    deferred = PyList_New(0);
+    if (!desc || !res || !blocked_pair || !blocked_space || !outs || !deferred) {
+        PyErr_NoMemory();
+        goto done;
+    }
+    uint8_t *hin = NULL, *hout = NULL;
+    if (n) {
+        qpp_session *s = session();
+        if (!s || check_rc(qpp_session_stage(s, total ? total : 1, (uint32_t)n, &hin, &hout)) < 0) goto done;
+        size_t off = 0;
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            PyObject *o = PyList_GetItem(packets, i);
+            const size_t l = (size_t)PyBytes_Size(o);
+            memcpy(hin + off, PyBytes_AsString(o), l);
+            qpp_desc *d = &desc[i];
+            d->in_off = d->out_off = off;
+            d->len = (uint32_t)l;
+            d->hdr_len = offs[i] > 0xffff ? 0xffff : (uint16_t)offs[i];
+            d->pn = exp[i];
+            d->slot = slots[i];
+            off += l;
+        }
+        if (host_call(0, kt, desc, (uint32_t)n, hin, total, hout, total, PyBytes_AsString(res)) < 0) goto done;
+    }
+    {
+        const qpp_result *r = (const qpp_result *)PyBytes_AsString(res);
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            const uint32_t p = pair[i], sp = space[i];
+            PyObject *item = Py_None;
+            Py_INCREF(Py_None);
+            PyList_SetItem(outs, i, item);
+            int defer = blocked_pair[p] || blocked_space[sp];
+            const uint16_t st = r[i].status;
+            const uint64_t now = sx[sp];
+            if (!defer && st == QPP_S_KEY_PHASE) defer = 1;
+            if (!defer && now != exp[i] && (st == QPP_S_OK || st == QPP_S_DECRYPT)) {
+                const int pn_len = (int)r[i].hdr_len - (int)offs[i];
+                if (pn_len < 1 || pn_len > 4 || decode_pn_signed(r[i].pn, pn_len, now) != (int64_t)r[i].pn) defer = 1;
+            }
+            if (defer) {
+                blocked_pair[p] = blocked_space[sp] = 1;
+                PyObject *ix = PyLong_FromSsize_t(i);
+                if (!ix || PyList_Append(deferred, ix) < 0) {
+                    Py_XDECREF(ix);
+                    goto done;
+                }
+                Py_DECREF(ix);
+                continue;
+            }
+            if (st != QPP_S_OK) continue;
+            const uint8_t *o = hout + desc[i].out_off;
+            PyObject *h = PyBytes_FromStringAndSize((const char *)o, r[i].hdr_len);
+            PyObject *pl = PyBytes_FromStringAndSize((const char *)o + r[i].hdr_len,
+                                                     (Py_ssize_t)r[i].out_len - r[i].hdr_len);
+            PyObject *pn = PyLong_FromUnsignedLongLong(r[i].pn);
+            item = (h && pl && pn) ? PyTuple_Pack(3, h, pl, pn) : NULL;
+            Py_XDECREF(h);
+            Py_XDECREF(pl);
+            Py_XDECREF(pn);
+            if (!item) goto done;
+            PyList_SetItem(outs, i, item);
+            if (track[i] && r[i].pn > now) sx[sp] = r[i].pn + 1;
+        }
+    }
+    ret = PyTuple_Pack(4, outs, res, deferred, sexp_out);
+done:
+    Py_XDECREF(sexp_out);
+    Py_XDECREF(outs);
+    Py_XDECREF(res);
+    Py_XDECREF(deferred);
+    free(desc);
+    free(blocked_pair);
+    free(blocked_space);
+    return ret;
+}
+
 static PyObject *py_hp_mask_host(PyObject *m, PyObject *args)
 {
     PyObject *t;
@@ -890,6 +1153,11 @@ static PyMethodDef module_methods[] = {
      "protect_list(table, slots_u32, pns_u64, headers, payloads) -> (wires, results)"},
     {"unprotect_list", py_unprotect_list, METH_VARARGS,
      "unprotect_list(table, slots_u32, expected_u64, packets, pn_offs_u32) -> (list of (header, payload) | None, results)"},
+    {"protect_datagrams", py_protect_datagrams, METH_VARARGS,
+     "protect_datagrams(table, plains, dg_u32, off_u32, hsize_u32, size_u32, pn_u64, slot_u32) -> (wires, results)"},
+    {"unprotect_walk", py_unprotect_walk, METH_VARARGS,
+     "unprotect_walk(table, slots_u32, exp_u64, packets, offs_u32, pair_u32, space_u32, track_u8, space_exp_u64, "
+     "n_pairs) -> (outcomes, results, deferred)"},
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},

@@ -30,7 +30,7 @@ from typing import Any, Callable, Optional, Sequence
 import numpy as np
 
 from . import layout as L
-from ._crypto import protect_host
+from ._crypto import protect_datagrams
 from .batch_io import KeySlots, _raise_status
 from .buffer import Buffer, size_uint_var
 from .tls import Epoch
@@ -80,16 +80,45 @@ _EPOCH_ONE_RTT = Epoch.ONE_RTT
 _MIN_PACKET_ROOM = 128
 
 
-@dataclass
 class _Pending:
-    """A closed packet awaiting encryption: where it sits in its datagram and
-    the key material it is to be protected with."""
+    """The closed packets of a builder awaiting encryption, one entry per
+    packet in flat lists: its datagram (index among the builder's closed
+    datagrams), offset in it, header size, plaintext header + payload size,
+    packet number, and the key material the reference would have encrypted
+    it with -- an index into `keys`, the builder's distinct (aead, hp,
+    key_phase) triples, so that slots are resolved per key, not per packet."""
 
-    offset: int
-    header_size: int
-    packet_size: int  # plaintext header + payload
-    packet_number: int
-    keys: tuple  # (aead, hp, key_phase) of the send context
+    __slots__ = ("dg", "off", "hsize", "size", "pn", "ref", "keys", "_key_ix")
+
+    def __init__(self) -> None:
+        self.dg: list = []
+        self.off: list = []
+        self.hsize: list = []
+        self.size: list = []
+        self.pn: list = []
+        self.ref: list = []
+        self.keys: list = []
+        self._key_ix: dict = {}
+
+    def __len__(self) -> int:
+        return len(self.dg)
+
+    def add(self, dg: int, off: int, hsize: int, size: int, pn: int, keys: tuple) -> None:
+        k = (id(keys[0]), id(keys[1]), keys[2])
+        r = self._key_ix.get(k)
+        if r is None:
+            r = self._key_ix[k] = len(self.keys)
+            self.keys.append(keys)
+        self.dg.append(dg)
+        self.off.append(off)
+        self.hsize.append(hsize)
+        self.size.append(size)
+        self.pn.append(pn & 0xFFFFFFFFFFFFFFFF)
+        self.ref.append(r)
+
+    def packets(self):
+        """(datagram, offset, header size, size, packet number, keys) per packet."""
+        return zip(self.dg, self.off, self.hsize, self.size, self.pn, (self.keys[r] for r in self.ref))
 
 
 _per_thread = threading.local()
@@ -120,9 +149,9 @@ class QuicPacketBuilder:
         self._quic_logger = quic_logger
         self._slots = slots
 
-        # finished datagrams (plaintext, tag holes) with their pending packets
+        # finished datagrams (plaintext, tag holes) and their pending packets
         self._datagrams: list = []
-        self._pending: list = []
+        self._pending = _Pending()
         self._packets: list = []
         self._flight_bytes = 0
         self._total_bytes = 0
@@ -134,7 +163,6 @@ class QuicPacketBuilder:
         self._datagram_fresh = True
         self._datagram_flight_bytes = 0
         self._datagram_needs_padding = False
-        self._datagram_pending: list = []
 
         # the packet being filled
         self._packet: Optional[QuicSentPacket] = None
@@ -277,8 +305,9 @@ class QuicPacketBuilder:
                 pair._update_key("local_update")
             ctx = getattr(pair, "send", pair)
             assert ctx.is_valid(), "Encryption key is not available"
-            self._datagram_pending.append(_Pending(self._packet_start, self._header_size, size,
-                                                   self._packet_number, (ctx.aead, ctx.hp, ctx.key_phase)))
+            # (the current datagram becomes datagram len(self._datagrams))
+            self._pending.add(len(self._datagrams), self._packet_start, self._header_size, size,
+                              self._packet_number, (ctx.aead, ctx.hp, ctx.key_phase))
             # leave the tag's room: the cursor ends where the reference's would
             buf.seek(self._packet_start + size)
             buf.push_bytes(bytes(pair.aead_tag_size))
@@ -304,8 +333,6 @@ class QuicPacketBuilder:
                 self._datagram_flight_bytes += extra
                 used += extra
         self._datagrams.append(buf.data)
-        self._pending.append(self._datagram_pending)
-        self._datagram_pending = []
         self._flight_bytes += self._datagram_flight_bytes
         self._total_bytes += used
         self._datagram_fresh = True
@@ -318,7 +345,7 @@ class QuicPacketBuilder:
             self._end_packet()
         self._flush_current_datagram()
         out = (self._datagrams, self._pending, self._packets)
-        self._datagrams, self._pending, self._packets = [], [], []
+        self._datagrams, self._pending, self._packets = [], _Pending(), []
         return out
 
     def flush(self) -> tuple:
@@ -332,8 +359,7 @@ def flush_builders(builders: Sequence[QuicPacketBuilder], slots: Optional[KeySlo
     builder order."""
     closed = [b._close() for b in builders]
     plains = [d for c in closed for d in c[0]]
-    pend = [p for c in closed for p in c[1]]
-    wire = _protect_datagrams(plains, pend, slots) if plains else []
+    wire = _protect_datagrams(plains, [(len(c[0]), c[1]) for c in closed], slots) if plains else []
     out, k = [], 0
     for dgrams, _, packets in closed:
         out.append((wire[k : k + len(dgrams)], packets))
@@ -343,29 +369,34 @@ def flush_builders(builders: Sequence[QuicPacketBuilder], slots: Optional[KeySlo
 
 def _protect_datagrams(plains: list, pending: list, slots: Optional[KeySlots]) -> list:
     """Encrypt every pending packet of the given plaintext datagrams in one
-    launch; the input and output share one layout (datagrams back to back,
-    packets at their offsets), so datagram d of the output is its wire form.
-    Bytes outside packets (datagram padding) are zeros in both."""
+    launch (_crypto.protect_datagrams: descriptors and pinned staging built in
+    C, one bytes object per wire datagram).  `pending` holds, per builder in
+    datagram order, (its datagram count, its _Pending).  The slots are
+    resolved once per distinct key of a builder."""
     slots = slots or _default_slots()
-    sizes = np.fromiter((len(d) for d in plains), np.int64, len(plains))
-    base = np.zeros(len(plains), np.int64)
-    np.cumsum(sizes[:-1], out=base[1:])
-    items = [(int(base[d]) + p.offset, p) for d, plist in enumerate(pending) for p in plist]
-    n = len(items)
-    desc = np.zeros(n, dtype=L.DESC)
-    if n:
-        off = np.fromiter((o for o, _ in items), np.int64, n)
-        desc["in_off"] = off
-        desc["out_off"] = off
-        desc["hdr_len"] = [p.header_size for _, p in items]
-        desc["len"] = [p.packet_size - p.header_size for _, p in items]
-        desc["pn"] = [p.packet_number & 0xFFFFFFFFFFFFFFFF for _, p in items]
-        desc["slot"] = slots.assign([p.keys for _, p in items])
-    total = int(sizes.sum())
-    wire, res = protect_host(slots.table, desc.tobytes(), b"".join(plains), total)
+    # every builder's distinct keys, assigned slots in one call
+    triples, firsts = [], []
+    for _, pend in pending:
+        firsts.append(len(triples))
+        triples += pend.keys
+    per_key = np.asarray(slots.assign(triples), dtype=np.uint32) if triples else np.zeros(0, np.uint32)
+    cols = {k: [] for k in ("dg", "off", "hsize", "size", "pn", "slot")}
+    base = 0
+    for (count, pend), first in zip(pending, firsts):
+        if len(pend):
+            cols["dg"].append(np.asarray(pend.dg, np.uint32) + np.uint32(base))
+            cols["off"].append(np.asarray(pend.off, np.uint32))
+            cols["hsize"].append(np.asarray(pend.hsize, np.uint32))
+            cols["size"].append(np.asarray(pend.size, np.uint32))
+            cols["pn"].append(np.asarray(pend.pn, np.uint64))
+            cols["slot"].append(per_key[first + np.asarray(pend.ref, np.int64)])
+        base += count
+    arr = {k: (np.concatenate(v) if v else np.zeros(0, np.uint64 if k == "pn" else np.uint32)).tobytes()
+           for k, v in cols.items()}
+    wire, res = protect_datagrams(slots.table, plains, arr["dg"], arr["off"], arr["hsize"], arr["size"],
+                                  arr["pn"], arr["slot"])
     status = np.frombuffer(res, dtype=L.RESULT)["status"]
-    bad = np.nonzero(status != L.S_OK)[0]
+    bad = np.flatnonzero(status != L.S_OK)
     if len(bad):
         raise _raise_status(int(status[bad[0]]))
-    mv = memoryview(wire)
-    return [bytes(mv[b : b + s]) for b, s in zip(base.tolist(), sizes.tolist())]
+    return wire

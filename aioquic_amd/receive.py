@@ -21,7 +21,7 @@ RFC 9000 sec. 12.2), no per-packet header parse.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, NamedTuple, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -73,8 +73,10 @@ class ConnectionKeys:
         return pair, space
 
 
-@dataclass
-class ReceivedPacket:
+class ReceivedPacket(NamedTuple):
+    """One packet's outcome, in datagram order (an immutable record; tuple
+    construction keeps the batched walk cheap per packet)."""
+
     datagram: int                 # index of the datagram in the batch
     offset: int                   # packet start within the datagram
     header: Optional[QuicHeader]  # None on the short-header fast path
@@ -90,16 +92,21 @@ class ReceivedPacket:
         return self.dropped is None
 
 
-def _walk_long(conn: ConnectionKeys, d: int, data: bytes, batch: ReceiveBatch, out: list, queued: list):
-    """One datagram through the header parser, packet by packet."""
+_new = tuple.__new__
+
+
+def _walk_long(conn: ConnectionKeys, d: int, data: bytes, out: list, queued: list, add) -> None:
+    """One datagram through the header parser, packet by packet.  Packets to
+    decrypt go to `add(pair, packet, encrypted_offset, space)` and their
+    record fields (datagram, offset, header, type, epoch) to `queued` with a
+    placeholder in `out`."""
     buf = Buffer(data=data)
     while not buf.eof():
         start = buf.tell()
         try:
             header = pull_quic_header(buf, host_cid_length=conn.host_cid_length)
         except ValueError:
-            out.append(ReceivedPacket(d, start, None, QuicPacketType.ONE_RTT, None,
-                                      dropped="header_parse_error"))
+            out.append(ReceivedPacket(d, start, None, QuicPacketType.ONE_RTT, None, dropped="header_parse_error"))
             return
         ptype = header.packet_type
         if not conn.is_client and ptype == QuicPacketType.INITIAL and len(data) < SMALLEST_MAX_DATAGRAM_SIZE:
@@ -123,37 +130,73 @@ def _walk_long(conn: ConnectionKeys, d: int, data: bytes, batch: ReceiveBatch, o
         enc_off = buf.tell() - start
         end = start + header.packet_length
         buf.seek(end)
-        out.append(ReceivedPacket(d, start, header, ptype, epoch))
-        queued.append(len(out) - 1)
-        batch.add(pair, data[start:end], enc_off, space=space)
+        queued.append((len(out), (d, start, header, ptype, epoch)))
+        out.append(None)
+        add(pair, data[start:end], enc_off, space)
 
 
 def receive_datagrams(items: Sequence[Tuple[ConnectionKeys, bytes]],
                       batch: Optional[ReceiveBatch] = None) -> List[ReceivedPacket]:
     """Parse and unprotect every packet of every (connection, datagram) in
     order; returns one ReceivedPacket per packet (or per dropped remainder of
-    a datagram, like the reference's early returns)."""
+    a datagram, like the reference's early returns).
+
+    Short-header datagrams (the 1-RTT bulk) skip the header parser: their
+    encrypted offset is 1 + the host CID length and the packet runs to the
+    end of the datagram.  Every packet goes into one ReceiveBatch, whose first
+    round (one launch and the in-order walk) runs in C."""
+    own = batch is None
     batch = batch or ReceiveBatch()
-    out: List[ReceivedPacket] = []
-    queued: List[int] = []
     if not items:
-        return out
+        return []
     first = np.fromiter((dg[0] if dg else 0 for _, dg in items), np.uint8, len(items))
-    short = (first & (PACKET_LONG_HEADER | PACKET_FIXED_BIT)) == PACKET_FIXED_BIT
-    for d, ((conn, data), is_short) in enumerate(zip(items, short.tolist())):
-        if is_short and len(data) > conn.host_cid_length:
-            pair, space = conn.pair_and_space(Epoch.ONE_RTT, None)
-            out.append(ReceivedPacket(d, 0, None, QuicPacketType.ONE_RTT, Epoch.ONE_RTT))
-            queued.append(len(out) - 1)
-            batch.add(pair, data, 1 + conn.host_cid_length, space=space)
+    short = ((first & (PACKET_LONG_HEADER | PACKET_FIXED_BIT)) == PACKET_FIXED_BIT).tolist()
+    out: list = []
+    queued: list = []  # (position in out, record fields) of every packet to decrypt
+    # runs of short-header datagrams go to the batch in bulk
+    r_pairs: list = []
+    r_packets: list = []
+    r_offs: list = []
+    r_spaces: list = []
+    by_conn: dict = {}
+    bulk = own or hasattr(batch, "_extend")
+
+    def flush_run():
+        if r_pairs:
+            if bulk:
+                batch._extend(r_pairs, r_packets, r_offs, r_spaces)
+            else:
+                for a, b, c, e in zip(r_pairs, r_packets, r_offs, r_spaces):
+                    batch.add(a, b, c, space=e)
+            r_pairs.clear(), r_packets.clear(), r_offs.clear(), r_spaces.clear()
+
+    def add(pair, packet, enc_off, space):
+        flush_run()
+        batch.add(pair, packet, enc_off, space=space)
+
+    one_rtt, ep1 = QuicPacketType.ONE_RTT, Epoch.ONE_RTT
+    for d, ((conn, data), is_short) in enumerate(zip(items, short)):
+        if is_short:
+            c = by_conn.get(id(conn))
+            if c is None:
+                pair, space = conn.pair_and_space(ep1, None)
+                c = by_conn[id(conn)] = (pair, space, 1 + conn.host_cid_length, conn)
+            if len(data) >= c[2]:
+                queued.append((len(out), (d, 0, None, one_rtt, ep1)))
+                out.append(None)
+                r_pairs.append(c[0])
+                r_packets.append(data)
+                r_offs.append(c[2])
+                r_spaces.append(c[1])
+                continue
+        _walk_long(conn, d, data, out, queued, add)
+    flush_run()
+    results = batch.run()
+    for (pos, f), res in zip(queued, results):
+        if isinstance(res, tuple):
+            out[pos] = _new(ReceivedPacket, f + res + (None,))
+        elif isinstance(res, KeyUnavailableError):
+            out[pos] = _new(ReceivedPacket, f + (b"", b"", -1, "key_unavailable"))
         else:
-            _walk_long(conn, d, data, batch, out, queued)
-    for k, res in zip(queued, batch.run()):
-        pkt = out[k]
-        if isinstance(res, KeyUnavailableError):
-            pkt.dropped = "key_unavailable"
-        elif isinstance(res, CryptoError):
-            pkt.dropped = "payload_decrypt_error"
-        else:
-            pkt.plain_header, pkt.plain_payload, pkt.packet_number = res
+            out[pos] = _new(ReceivedPacket, f + (b"", b"", -1, "payload_decrypt_error"))
     return out

@@ -58,19 +58,23 @@ class _Pair:
 
 
 def _oracle_protect(oracle):
+    """Stand-in for packet_builder._protect_datagrams: each pending packet
+    protected by the oracle.  pending = [(datagram count, _Pending)] per
+    builder, as flush_builders passes it."""
     def protect(plains, pending, slots):
-        out = []
-        for dg, plist in zip(plains, pending):
-            d = bytearray(dg)
-            for p in plist:
-                suite, key, iv = p.keys[0]._material()
-                _, hp = p.keys[1]._material()
-                hdr = bytes(d[p.offset : p.offset + p.header_size])
-                pay = bytes(d[p.offset + p.header_size : p.offset + p.packet_size])
-                wire = oracle.protect(suite, key, iv, hp, hdr, pay, p.packet_number)
-                d[p.offset : p.offset + len(wire)] = wire
-            out.append(bytes(d))
-        return out
+        out = [bytearray(d) for d in plains]
+        base = 0
+        for count, pend in pending:
+            for dg, off, hsize, size, pn, keys in pend.packets():
+                d = out[base + dg]
+                suite, key, iv = keys[0]._material()
+                _, hp = keys[1]._material()
+                hdr = bytes(d[off : off + hsize])
+                pay = bytes(d[off + hsize : off + size])
+                wire = oracle.protect(suite, key, iv, hp, hdr, pay, pn)
+                d[off : off + len(wire)] = wire
+            base += count
+        return [bytes(d) for d in out]
 
     return protect
 
@@ -281,7 +285,7 @@ def test_flush_builders_matches_oracle(oracle):
     got = PB.flush_builders(builders)
     for (dgrams, packets), twin in zip(got, twins):
         plains, pending, tpackets = twin._close()
-        want = _oracle_protect(oracle)(plains, pending, None)
+        want = _oracle_protect(oracle)(plains, [(len(plains), pending)], None)
         assert [len(d) for d in dgrams] == [len(d) for d in want]
         assert dgrams == want
         assert [p.sent_bytes for p in packets] == [p.sent_bytes for p in tpackets]
@@ -303,7 +307,7 @@ def test_flush_builders_two_threads(oracle):
                 got = PB.flush_builders(builders)
                 for (dgrams, _), twin in zip(got, twins):
                     plains, pending, _ = twin._close()
-                    if dgrams != _oracle_protect(oracle)(plains, pending, None):
+                    if dgrams != _oracle_protect(oracle)(plains, [(len(plains), pending)], None):
                         errors.append((tag, rep))
             results[tag] = True
         except Exception as e:  # noqa: BLE001 - reported below
