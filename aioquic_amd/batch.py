@@ -22,7 +22,7 @@ import numpy as np
 from . import layout as L
 from . import _crypto
 
-__all__ = ["PacketEngine", "KeySpec", "layout_packets"]
+__all__ = ["PacketEngine", "MultiDeviceEngine", "KeySpec", "layout_packets"]
 
 
 @dataclass
@@ -143,6 +143,35 @@ class PacketEngine:
         # the arrays stay referenced here for the whole call
         fn(self.table, desc.ctypes.data, len(desc), data.ctypes.data, data.nbytes,
            out.ctypes.data, out.nbytes, results.ctypes.data)
+
+
+class MultiDeviceEngine:
+    """Host-buffer batches split over several GPUs of the node (qpp_multi):
+    the batch's descriptors are cut into contiguous ranges, one per device,
+    each device holds its own replica of the key table and its own pinned
+    staging, and the results come back in the caller's order -- the bytes of
+    PacketEngine.protect_host on one device.  `devices` defaults to every
+    visible GPU; a device may be listed twice (two sessions on one GPU)."""
+
+    def __init__(self, capacity: int, devices=None):
+        if devices is None:
+            import torch
+
+            devices = list(range(torch.cuda.device_count()))
+        self.devices = list(devices)
+        self.multi = _crypto.MultiSession(self.devices, int(capacity))
+
+    def set_key_records(self, recs: np.ndarray) -> None:
+        assert recs.dtype == L.KEY_MATERIAL
+        self.multi.set_keys(np.ascontiguousarray(recs).tobytes())
+
+    def protect_host(self, desc: np.ndarray, data, out_len: int):
+        out, res = self.multi.protect(np.ascontiguousarray(desc).tobytes(), bytes(data), int(out_len))
+        return np.frombuffer(out, dtype=np.uint8), np.frombuffer(res, dtype=L.RESULT)
+
+    def unprotect_host(self, desc: np.ndarray, data, out_len: int):
+        out, res = self.multi.unprotect(np.ascontiguousarray(desc).tobytes(), bytes(data), int(out_len))
+        return np.frombuffer(out, dtype=np.uint8), np.frombuffer(res, dtype=L.RESULT)
 
 
 def layout_packets(headers, payloads, pns, slots, *, align: int = 1, tag_room: bool = True,

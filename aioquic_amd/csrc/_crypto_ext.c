@@ -26,6 +26,8 @@
  *   protect_into(table, desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr) -> None
  *   unprotect_into(...)                                                         -> None
  *   hp_mask_host(table, slots, samples) -> bytes
+ *   protect_datagrams(...), unprotect_walk(...)     the batched callers' C paths
+ *   MultiSession(devices, key_capacity)             one host batch over several GPUs
  *
  * Threads: host-buffer calls release the GIL.  Each OS thread gets its own
  * qpp_session (pinned staging + streams; quic_pp.h: a session is single-
@@ -42,7 +44,7 @@
 #include "quic_pp.h"
 
 static PyObject *g_crypto_error;
-static PyObject *g_aead_type, *g_hp_type, *g_kt_type, *g_plan_type;
+static PyObject *g_aead_type, *g_hp_type, *g_kt_type, *g_plan_type, *g_multi_type;
 
 /* ------------------------------------------------------------ sessions -- */
 
@@ -582,6 +584,136 @@ static int as_plan(PyObject *o, qpp_plan **out)
     *out = ((PlanObject *)o)->plan;
     return 0;
 }
+
+/* --------------------------------------------------------- MultiSession -- */
+
+/* MultiSession(devices, key_capacity): one host batch over several GPUs
+ * (qpp_multi, quic_pp.h).  .set_keys(materials), .protect(desc, data,
+ * out_len) / .unprotect(...) -> (out, results) like protect_host; .devices. */
+typedef struct {
+    PyObject_HEAD
+    qpp_multi *m;
+} MultiObject;
+
+static int Multi_init(MultiObject *self, PyObject *args, PyObject *kwargs)
+{
+    PyObject *devs;
+    unsigned int cap;
+    if (!PyArg_ParseTuple(args, "OI", &devs, &cap)) return -1;
+    const Py_ssize_t nd = PySequence_Size(devs);
+    int ids[16];
+    if (nd < 0) return -1;
+    if (nd < 1 || nd > 16) {
+        PyErr_SetString(PyExc_ValueError, "1 to 16 devices");
+        return -1;
+    }
+    for (Py_ssize_t k = 0; k < nd; ++k) {
+        PyObject *it = PySequence_GetItem(devs, k);
+        if (!it) return -1;
+        ids[k] = (int)PyLong_AsLong(it);
+        Py_DECREF(it);
+        if (ids[k] == -1 && PyErr_Occurred()) return -1;
+    }
+    if (self->m) {
+        qpp_multi_destroy(self->m);
+        self->m = NULL;
+    }
+    int rc = qpp_multi_create(ids, (int)nd, cap, &self->m);
+    if (rc == QPP_E_ARG) {
+        PyErr_SetString(PyExc_ValueError, "bad device list or key capacity");
+        return -1;
+    }
+    return check_rc(rc);
+}
+
+static void Multi_dealloc(MultiObject *self)
+{
+    if (self->m) qpp_multi_destroy(self->m);
+    heap_dealloc((PyObject *)self);
+}
+
+static PyObject *Multi_set_keys(MultiObject *self, PyObject *args)
+{
+    const char *b;
+    Py_ssize_t len;
+    if (!PyArg_ParseTuple(args, "y#", &b, &len)) return NULL;
+    if (len % (Py_ssize_t)sizeof(qpp_key_material)) {
+        PyErr_SetString(PyExc_ValueError, "materials must be a whole number of 84-byte records");
+        return NULL;
+    }
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = qpp_multi_set_keys(self->m, (const qpp_key_material *)b, (uint32_t)(len / (Py_ssize_t)sizeof(qpp_key_material)));
+    Py_END_ALLOW_THREADS
+    if (rc == QPP_E_ARG) {
+        PyErr_SetString(PyExc_ValueError, "bad key material (slot out of range or unknown suite)");
+        return NULL;
+    }
+    if (check_rc(rc) < 0) return NULL;
+    Py_RETURN_NONE;
+}
+
+static PyObject *multi_run_py(MultiObject *self, PyObject *args, int enc)
+{
+    const char *desc, *data;
+    Py_ssize_t desc_len, data_len, out_len;
+    if (!PyArg_ParseTuple(args, "y#y#n", &desc, &desc_len, &data, &data_len, &out_len)) return NULL;
+    if (desc_len % (Py_ssize_t)sizeof(qpp_desc) || out_len < 0) {
+        PyErr_SetString(PyExc_ValueError, "bad descriptor buffer or output length");
+        return NULL;
+    }
+    const uint32_t n = (uint32_t)(desc_len / (Py_ssize_t)sizeof(qpp_desc));
+    PyObject *out = PyBytes_FromStringAndSize(NULL, out_len);
+    PyObject *res = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)n * (Py_ssize_t)sizeof(qpp_result));
+    PyObject *ret = NULL;
+    if (out && res) {
+        int rc;
+        char *o = PyBytes_AsString(out), *r = PyBytes_AsString(res);
+        Py_BEGIN_ALLOW_THREADS
+        rc = enc ? qpp_multi_protect(self->m, (const qpp_desc *)desc, n, (const uint8_t *)data, (size_t)data_len,
+                                     (uint8_t *)o, (size_t)out_len, (qpp_result *)r)
+                 : qpp_multi_unprotect(self->m, (const qpp_desc *)desc, n, (const uint8_t *)data, (size_t)data_len,
+                                       (uint8_t *)o, (size_t)out_len, (qpp_result *)r);
+        Py_END_ALLOW_THREADS
+        if (check_rc(rc) == 0) ret = PyTuple_Pack(2, out, res);
+    }
+    Py_XDECREF(out);
+    Py_XDECREF(res);
+    return ret;
+}
+
+static PyObject *Multi_protect(MultiObject *self, PyObject *args) { return multi_run_py(self, args, 1); }
+static PyObject *Multi_unprotect(MultiObject *self, PyObject *args) { return multi_run_py(self, args, 0); }
+
+static PyObject *Multi_devices(MultiObject *self, void *unused)
+{
+    return PyLong_FromLong(qpp_multi_devices(self->m));
+}
+
+static PyMethodDef Multi_methods[] = {
+    {"set_keys", (PyCFunction)Multi_set_keys, METH_VARARGS, "set_keys(materials) on every device"},
+    {"protect", (PyCFunction)Multi_protect, METH_VARARGS, "protect(desc, data, out_len) -> (out, results)"},
+    {"unprotect", (PyCFunction)Multi_unprotect, METH_VARARGS, "unprotect(desc, data, out_len) -> (out, results)"},
+    {NULL},
+};
+
+static PyGetSetDef Multi_getset[] = {
+    {"devices", (getter)Multi_devices, NULL, "number of device sessions", NULL},
+    {NULL},
+};
+
+static PyType_Slot Multi_slots[] = {
+    {Py_tp_doc, "one host batch over several GPUs (qpp_multi)"},
+    {Py_tp_methods, Multi_methods},
+    {Py_tp_getset, Multi_getset},
+    {Py_tp_init, Multi_init},
+    {Py_tp_new, PyType_GenericNew},
+    {Py_tp_dealloc, Multi_dealloc},
+    {0, NULL},
+};
+
+static PyType_Spec Multi_spec = {"aioquic_amd._crypto.MultiSession", sizeof(MultiObject), 0,
+                                 Py_TPFLAGS_DEFAULT, Multi_slots};
 
 /* -------------------------------------------------------- batch calls -- */
 
@@ -1189,7 +1321,8 @@ PyMODINIT_FUNC PyInit__crypto(void)
     if (add_type(m, &AEAD_spec, "AEAD", &g_aead_type) < 0 ||
         add_type(m, &HP_spec, "HeaderProtection", &g_hp_type) < 0 ||
         add_type(m, &KT_spec, "KeyTable", &g_kt_type) < 0 ||
-        add_type(m, &Plan_spec, "Plan", &g_plan_type) < 0)
+        add_type(m, &Plan_spec, "Plan", &g_plan_type) < 0 ||
+        add_type(m, &Multi_spec, "MultiSession", &g_multi_type) < 0)
         return NULL;
     PyModule_AddIntConstant(m, "DESC_SIZE", (long)sizeof(qpp_desc));
     PyModule_AddIntConstant(m, "RESULT_SIZE", (long)sizeof(qpp_result));

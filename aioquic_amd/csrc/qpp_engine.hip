@@ -1566,7 +1566,9 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <thread>
+#include <vector>
 
 using namespace qpp;
 
@@ -1604,6 +1606,7 @@ static uint32_t keytab_suite_mask(const qpp_keytab *kt)
 // session_run_pipelined).
 constexpr size_t kPipeChunkBytes = (size_t)32 << 20;
 constexpr int kPipeMaxChunks = 32;
+constexpr int kMultiMaxDevices = 16;  // qpp_multi: devices per host-batch engine
 
 struct qpp_session {
     hipStream_t stream;             // kernels (and everything of the serial path)
@@ -2314,6 +2317,188 @@ int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material 
 {
     if (!s) return QPP_E_ARG;
     return qpp_keytab_set(kt, km, n, s->stream);
+}
+
+// ------------------------------------------------------ several devices --
+//
+// One host batch over several GPUs of the node (packets
+// are independent, so no collective): a session and a replica of the key
+// table per device; the batch is cut into contiguous descriptor ranges, one
+// per device, each range's input and output extents are staged and run by its
+// own host thread on its own device, and every result lands at its packet's
+// position in the caller's arrays.  Each range needs its own output extent,
+// so the ranges' output extents must not overlap (descriptors in output
+// order, the layout of a socket batch); otherwise the batch runs on the first
+// device alone.  Output bytes outside every packet are zeros, as for one
+// session.
+
+struct qpp_multi {
+    int n;
+    int device[kMultiMaxDevices];
+    qpp_session *s[kMultiMaxDevices];
+    qpp_keytab *kt[kMultiMaxDevices];
+};
+
+int qpp_multi_create(const int *devices, int n_devices, uint32_t key_capacity, qpp_multi **out)
+{
+    if (!out || !devices || n_devices < 1 || n_devices > kMultiMaxDevices) return QPP_E_ARG;
+    *out = NULL;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) return QPP_E_NODEV;
+    for (int k = 0; k < n_devices; ++k)
+        if (devices[k] < 0 || devices[k] >= count) return QPP_E_ARG;
+    qpp_multi *m = (qpp_multi *)calloc(1, sizeof(qpp_multi));
+    if (!m) return QPP_E_NOMEM;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    int rc = QPP_OK;
+    for (int k = 0; k < n_devices && rc == QPP_OK; ++k) {
+        m->device[k] = devices[k];
+        if (hipSetDevice(devices[k]) != hipSuccess) rc = QPP_E_HIP;
+        if (rc == QPP_OK) rc = qpp_session_create(1 << 16, 64, &m->s[k]);
+        if (rc == QPP_OK) rc = qpp_keytab_create(key_capacity, &m->kt[k]);
+        m->n = k + 1;
+    }
+    (void)hipSetDevice(prev);
+    if (rc != QPP_OK) {
+        qpp_multi_destroy(m);
+        return rc;
+    }
+    *out = m;
+    return QPP_OK;
+}
+
+void qpp_multi_destroy(qpp_multi *m)
+{
+    if (!m) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    for (int k = 0; k < m->n; ++k) {
+        (void)hipSetDevice(m->device[k]);
+        qpp_session_destroy(m->s[k]);
+        qpp_keytab_destroy(m->kt[k]);
+    }
+    (void)hipSetDevice(prev);
+    free(m);
+}
+
+int qpp_multi_devices(const qpp_multi *m) { return m ? m->n : 0; }
+
+int qpp_multi_set_keys(qpp_multi *m, const qpp_key_material *km, uint32_t n)
+{
+    if (!m) return QPP_E_ARG;
+    int prev = 0, rc = QPP_OK;
+    (void)hipGetDevice(&prev);
+    for (int k = 0; k < m->n && rc == QPP_OK; ++k) {
+        if (hipSetDevice(m->device[k]) != hipSuccess) rc = QPP_E_HIP;
+        if (rc == QPP_OK) rc = qpp_session_set_keys(m->s[k], m->kt[k], km, n);
+        if (rc == QPP_OK) rc = hipStreamSynchronize((hipStream_t)qpp_session_stream(m->s[k])) == hipSuccess
+                                   ? QPP_OK : QPP_E_HIP;
+    }
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+static int multi_run(bool enc, qpp_multi *m, const qpp_desc *desc, uint32_t n, const uint8_t *in,
+                     size_t in_len, uint8_t *out, size_t out_len, qpp_result *res)
+{
+    if (!m || (n && (!desc || !res))) return QPP_E_ARG;
+    if (n == 0) {
+        if (out_len) memset(out, 0, out_len);
+        return QPP_OK;
+    }
+    int parts = m->n < (int)n ? m->n : (int)n;
+    // bounds first (as a session does), so that extents use only packets
+    // that fit; rejected ones keep offset 0 in their range and touch nothing
+    std::vector<qpp_desc> d(desc, desc + n);
+    reject_out_of_bounds(enc, d.data(), n, in_len, out_len);
+    struct Range {
+        uint32_t b, e;
+        size_t ilo, ihi, olo, ohi;
+    };
+    std::vector<Range> r(parts);
+    for (int k = 0; k < parts; ++k) {
+        Range &x = r[k];
+        x.b = (uint32_t)((uint64_t)n * k / parts);
+        x.e = (uint32_t)((uint64_t)n * (k + 1) / parts);
+        x.ilo = x.olo = SIZE_MAX;
+        x.ihi = x.ohi = 0;
+        for (uint32_t i = x.b; i < x.e; ++i) {
+            if (d[i].flags & kFlagReject) continue;
+            const size_t rd = enc ? (size_t)d[i].hdr_len + d[i].len : d[i].len;
+            const size_t wr = enc ? rd + QPP_TAG_LEN : rd;
+            x.ilo = std::min<size_t>(x.ilo, d[i].in_off);
+            x.ihi = std::max<size_t>(x.ihi, d[i].in_off + rd);
+            x.olo = std::min<size_t>(x.olo, d[i].out_off);
+            x.ohi = std::max<size_t>(x.ohi, d[i].out_off + wr);
+        }
+        if (x.ilo == SIZE_MAX) x.ilo = x.ihi = x.olo = x.ohi = 0;
+    }
+    // ranges in output order with disjoint extents, or one device
+    for (int k = 1; k < parts; ++k)
+        if (r[k].ohi > r[k].olo && r[k - 1].ohi > r[k].olo) {
+            parts = 1;
+            r.assign(1, Range{0, n, 0, in_len, 0, out_len});
+            break;
+        }
+    if (parts == 1) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(m->device[0]);
+        const int rc = enc ? qpp_session_protect(m->s[0], m->kt[0], desc, n, in, in_len, out, out_len, res)
+                           : qpp_session_unprotect(m->s[0], m->kt[0], desc, n, in, in_len, out, out_len, res);
+        (void)hipSetDevice(prev);
+        return rc;
+    }
+    // rebase each range onto its extents
+    for (int k = 0; k < parts; ++k)
+        for (uint32_t i = r[k].b; i < r[k].e; ++i) {
+            if (d[i].flags & kFlagReject) {
+                d[i].in_off = d[i].out_off = 0;
+                continue;
+            }
+            d[i].in_off -= r[k].ilo;
+            d[i].out_off -= r[k].olo;
+        }
+    // output bytes outside every range's extent: zeros, as one session leaves them
+    size_t pos = 0;
+    for (int k = 0; k < parts; ++k) {
+        if (r[k].ohi <= r[k].olo) continue;
+        if (r[k].olo > pos) memset(out + pos, 0, r[k].olo - pos);
+        pos = r[k].ohi;
+    }
+    if (out_len > pos) memset(out + pos, 0, out_len - pos);
+    std::vector<int> rcs(parts, QPP_OK);
+    std::vector<std::thread> th;
+    for (int k = 0; k < parts; ++k)
+        th.emplace_back([&, k] {
+            const Range &x = r[k];
+            if (hipSetDevice(m->device[k]) != hipSuccess) {
+                rcs[k] = QPP_E_HIP;
+                return;
+            }
+            const uint32_t cnt = x.e - x.b;
+            rcs[k] = enc ? qpp_session_protect(m->s[k], m->kt[k], d.data() + x.b, cnt, in + x.ilo, x.ihi - x.ilo,
+                                               out + x.olo, x.ohi - x.olo, res + x.b)
+                         : qpp_session_unprotect(m->s[k], m->kt[k], d.data() + x.b, cnt, in + x.ilo, x.ihi - x.ilo,
+                                                 out + x.olo, x.ohi - x.olo, res + x.b);
+        });
+    for (auto &t : th) t.join();
+    for (int k = 0; k < parts; ++k)
+        if (rcs[k] != QPP_OK) return rcs[k];
+    return QPP_OK;
+}
+
+int qpp_multi_protect(qpp_multi *m, const qpp_desc *desc, uint32_t n, const uint8_t *in, size_t in_len,
+                      uint8_t *out, size_t out_len, qpp_result *res)
+{
+    return multi_run(true, m, desc, n, in, in_len, out, out_len, res);
+}
+
+int qpp_multi_unprotect(qpp_multi *m, const qpp_desc *desc, uint32_t n, const uint8_t *in, size_t in_len,
+                        uint8_t *out, size_t out_len, qpp_result *res)
+{
+    return multi_run(false, m, desc, n, in, in_len, out, out_len, res);
 }
 
 }  // extern "C"

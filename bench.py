@@ -562,6 +562,8 @@ def main():
             out["e2e"] = e2e(PacketEngine, cfg, seed, dev, args.e2e_packets,
                              chunks=args.e2e_chunks, n_streams=args.e2e_streams,
                              mode=args.e2e_mode)
+            if world == 1:
+                out["e2e_host_devices"] = e2e_host_devices(cfg, seed, args.e2e_packets)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -575,6 +577,36 @@ def _workload_name(cfg, n):
     def ki(x):
         return f"{x >> 20}Mi" if x % (1 << 20) == 0 else f"{x >> 10}Ki" if x % 1024 == 0 else str(x)
     return cfg["name"].replace(ki(cfg["n"]), ki(n), 1)
+
+
+def e2e_host_devices(cfg, seed, n, reps=3):
+    """The library's own host-buffer path over every visible GPU
+    (MultiDeviceEngine / qpp_multi: one host batch cut into contiguous ranges,
+    one session and key-table replica per device, host threads in parallel):
+    host memory -> protect -> host, then host -> unprotect -> host, per device
+    count 1..D.  PCIe-inclusive; never the bench value."""
+    import torch
+    from aioquic_amd.batch import MultiDeviceEngine
+    from aioquic_amd.bench_data import make_workload
+
+    w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=seed, version=cfg["version"],
+                      mixed=cfg.get("mixed"))
+    out = {}
+    for d in range(1, torch.cuda.device_count() + 1):
+        eng = MultiDeviceEngine(w.n_keys, devices=list(range(d)))
+        eng.set_key_records(w.keys)
+        wire, _ = eng.protect_host(w.desc, w.plain, w.wire_size)  # warm-up (staging allocation)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            wire, r1 = eng.protect_host(w.desc, w.plain, w.wire_size)
+            back, r2 = eng.unprotect_host(w.udesc, wire, w.plain_size)
+            times.append(time.perf_counter() - t0)
+        ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all() and np.array_equal(back, w.plain))
+        out[str(d)] = {"gib_s": round(n * 1200 / float(np.median(times)) / GIB, 3), "round_trip_ok": ok}
+        del eng
+    return {"per_device_count": out, "packets": n,
+            "note": "host bytes -> qpp_multi protect -> host, host -> unprotect -> host (two synchronous calls)"}
 
 
 def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5, mode="staged"):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define QPP_ABI_VERSION 2
+#define QPP_ABI_VERSION 3
 
 /* cipher suites (quic/crypto.py:12-16 CIPHER_SUITES) */
 #define QPP_AES_128_GCM 0        /* aes-128-gcm + aes-128-ecb header protection */
@@ -217,6 +217,26 @@ int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *sl
 int qpp_session_stage(qpp_session *s, size_t bytes, uint32_t n, uint8_t **h_in, uint8_t **h_out);
 int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material *km,
                          uint32_t n);
+
+/* One host batch over several GPUs of the node (the
+ * server socket of src/aioquic/asyncio/server.py:60-152 feeds all
+ * connections, and that is the batch to split).  A qpp_multi holds a session
+ * and a replica of the key table per device; *_protect / *_unprotect cut the
+ * batch into contiguous descriptor ranges, one per device, run them at once
+ * (one host thread each) and write every result at its packet's position in
+ * the caller's arrays -- the same bytes and results as one session.  Ranges
+ * need disjoint output extents (descriptors in output order); otherwise the
+ * batch runs on the first device.  Up to 16 devices; a device may be listed
+ * twice (two sessions on one GPU).  Like a session, single-threaded. */
+typedef struct qpp_multi qpp_multi;
+int qpp_multi_create(const int *devices, int n_devices, uint32_t key_capacity, qpp_multi **out);
+void qpp_multi_destroy(qpp_multi *m);
+int qpp_multi_devices(const qpp_multi *m);
+int qpp_multi_set_keys(qpp_multi *m, const qpp_key_material *km, uint32_t n);
+int qpp_multi_protect(qpp_multi *m, const qpp_desc *desc, uint32_t n, const uint8_t *in, size_t in_len,
+                      uint8_t *out, size_t out_len, qpp_result *res);
+int qpp_multi_unprotect(qpp_multi *m, const qpp_desc *desc, uint32_t n, const uint8_t *in, size_t in_len,
+                        uint8_t *out, size_t out_len, qpp_result *res);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,64 @@
+"""Library-level multi-device host path (qpp_multi, aioquic_amd.batch.MultiDeviceEngine).
+
+One host batch split into contiguous ranges, one session and key-table
+replica per device; on the one-GPU box the "devices" are sessions on the same
+GPU.  The bytes and results must equal one session's (PacketEngine) and the
+oracle's, for protect and unprotect, mixed suites, rejected descriptors, and
+a layout whose ranges would overlap (run on one device)."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _workload(n, seed):
+    from aioquic_amd import bench_data
+
+    return bench_data.make_workload(n, suite=0, n_keys=6, seed=seed, mixed=(0, 1, 2))
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]], ids=["2-sessions", "3-sessions"])
+def test_multi_equals_single_session(oracle, devices):
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import MultiDeviceEngine, PacketEngine
+
+    w = _workload(3001, 0x51)
+    one = PacketEngine(w.n_keys)
+    one.set_key_records(w.keys)
+    multi = MultiDeviceEngine(w.n_keys, devices=devices)
+    assert multi.multi.devices == len(devices)
+    multi.set_key_records(w.keys)
+    wire1, r1 = one.protect_host(w.desc, w.plain, w.wire_size)
+    wire2, r2 = multi.protect_host(w.desc, w.plain, w.wire_size)
+    assert (r1["status"] == L.S_OK).all()
+    assert np.array_equal(wire1, wire2) and np.array_equal(r1, r2)
+    exp, _ = oracle.protect_batch(w.keys, w.desc, w.plain, w.wire_size)
+    assert np.array_equal(wire2, exp)
+    back1, u1 = one.unprotect_host(w.udesc, wire1, w.plain_size)
+    back2, u2 = multi.unprotect_host(w.udesc, wire2, w.plain_size)
+    assert np.array_equal(back1, back2) and np.array_equal(u1, u2)
+    assert np.array_equal(back2, w.plain)
+
+
+def test_multi_rejects_and_overlap_like_one_session():
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import MultiDeviceEngine, PacketEngine
+
+    w = _workload(800, 0x52)
+    one = PacketEngine(w.n_keys)
+    one.set_key_records(w.keys)
+    multi = MultiDeviceEngine(w.n_keys, devices=[0, 0])
+    multi.set_key_records(w.keys)
+    d = w.desc.copy()
+    d[5]["in_off"] = w.plain_size + 10  # outside the input: QPP_S_LENGTH, nothing touched
+    d[600]["out_off"] = w.wire_size - 3  # output past the end
+    a = one.protect_host(d, w.plain, w.wire_size)
+    b = multi.protect_host(d, w.plain, w.wire_size)
+    assert a[1][5]["status"] == L.S_LENGTH and a[1][600]["status"] == L.S_LENGTH
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    # descriptors out of output order: the ranges' extents overlap -> one device
+    rev = w.desc[::-1].copy()
+    a = one.protect_host(rev, w.plain, w.wire_size)
+    b = multi.protect_host(rev, w.plain, w.wire_size)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
