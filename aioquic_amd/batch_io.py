@@ -33,6 +33,7 @@ step (quic/connection.py:905-947, CryptoPair.decrypt_packet, crypto.py:184-192).
 
 from __future__ import annotations
 
+import threading
 import weakref
 from typing import Optional, Union
 
@@ -146,6 +147,19 @@ def _release_keys(*objs) -> None:
 
 
 crypto_mod._KEY_RELEASE_HOOKS.append(_release_keys)
+
+_per_thread = threading.local()
+
+
+def default_slots() -> KeySlots:
+    """The batched callers' default key table (the builders' flush and
+    receive_datagrams): one per OS thread, so concurrent batches on different
+    threads never assign or reset each other's slots (the C extension gives
+    each thread its own staging the same way)."""
+    t = getattr(_per_thread, "slots", None)
+    if t is None:
+        t = _per_thread.slots = KeySlots(4096)
+    return t
 
 
 def _raise_status(status: int) -> Exception:

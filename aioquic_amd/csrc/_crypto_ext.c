@@ -120,6 +120,58 @@ static int hp_suite(const char *name, Py_ssize_t len)
 
 static int suite_key_len(int suite) { return suite == QPP_AES_128_GCM ? 16 : 32; }
 
+/* --------------------------------------------------- parallel host copy -- */
+
+/* Many (dst, src, len) copies between caller memory and pinned staging, split
+ * over up to 8 threads by bytes (one thread streams ~6-10 GB/s, well under
+ * the PCIe rate).  Small totals stay on the calling thread.  Call without the
+ * GIL only when every buffer is kept alive by the caller. */
+typedef struct {
+    uint8_t **dst;
+    const uint8_t **src;
+    const size_t *len;
+    size_t b, e;
+} CopyJob;
+
+static void *copy_job(void *arg)
+{
+    CopyJob *j = (CopyJob *)arg;
+    for (size_t i = j->b; i < j->e; ++i) memcpy(j->dst[i], j->src[i], j->len[i]);
+    return NULL;
+}
+
+static void par_copy(uint8_t **dst, const uint8_t **src, const size_t *len, size_t n, size_t total)
+{
+    enum { kThreads = 8 };
+    const size_t kMin = (size_t)4 << 20;
+    int parts = total >= kMin ? (int)(total / (kMin / 2)) : 1;
+    if (parts > kThreads) parts = kThreads;
+    if (parts < 2 || n < 2) {
+        CopyJob j = {dst, src, len, 0, n};
+        copy_job(&j);
+        return;
+    }
+    CopyJob jobs[kThreads];
+    pthread_t th[kThreads];
+    int started[kThreads] = {0};
+    size_t i = 0, acc = 0;
+    for (int t = 0; t < parts; ++t) {
+        const size_t goal = total / parts * (size_t)(t + 1);
+        jobs[t].dst = dst;
+        jobs[t].src = src;
+        jobs[t].len = len;
+        jobs[t].b = i;
+        while (i < n && (acc < goal || t == parts - 1)) acc += len[i++];
+        jobs[t].e = i;
+    }
+    for (int t = 1; t < parts; ++t) started[t] = pthread_create(&th[t], NULL, copy_job, &jobs[t]) == 0;
+    copy_job(&jobs[0]);
+    for (int t = 1; t < parts; ++t) {
+        if (started[t]) pthread_join(th[t], NULL);
+        else copy_job(&jobs[t]);
+    }
+}
+
 /* ------------------------------------------------------------ key slot -- */
 
 /* A single-slot device key table, created on first use.  The slot is
@@ -1049,24 +1101,48 @@ static PyObject *py_protect_datagrams(PyObject *m, PyObject *args)
         uint8_t *hin, *hout;
         if (!s || check_rc(qpp_session_stage(s, total ? total : 1, (uint32_t)(n ? n : 1), &hin, &hout)) < 0)
             goto done;
-        for (Py_ssize_t d = 0; d < nd; ++d)
-            memcpy(hin + base[d], PyBytes_AsString(PyList_GetItem(plains, d)), base[d + 1] - base[d]);
+        /* the copy jobs: datagram d between its bytes object and staging */
+        uint8_t **cd = (uint8_t **)malloc(((size_t)nd + 1) * sizeof(uint8_t *));
+        const uint8_t **cs = (const uint8_t **)malloc(((size_t)nd + 1) * sizeof(uint8_t *));
+        size_t *cl = (size_t *)malloc(((size_t)nd + 1) * sizeof(size_t));
+        if (!cd || !cs || !cl) {
+            free(cd), free(cs), free(cl);
+            PyErr_NoMemory();
+            goto done;
+        }
+        for (Py_ssize_t d = 0; d < nd; ++d) {
+            cd[d] = hin + base[d];
+            cs[d] = (const uint8_t *)PyBytes_AsString(PyList_GetItem(plains, d));
+            cl[d] = base[d + 1] - base[d];
+        }
+        Py_BEGIN_ALLOW_THREADS  /* the list holds every datagram */
+        par_copy(cd, cs, cl, (size_t)nd, total);
+        Py_END_ALLOW_THREADS
         const uint8_t *src = hin;  /* no packet: the datagrams as they are */
+        int ok = 1;
         if (n) {
-            if (host_call(1, kt, desc, (uint32_t)n, hin, total, hout, total, PyBytes_AsString(res)) < 0) goto done;
+            ok = host_call(1, kt, desc, (uint32_t)n, hin, total, hout, total, PyBytes_AsString(res)) == 0;
             src = hout;
         }
-        wires = PyList_New(nd);
-        if (!wires) goto done;
-        for (Py_ssize_t d = 0; d < nd; ++d) {
-            PyObject *o = PyBytes_FromStringAndSize((const char *)src + base[d], (Py_ssize_t)(base[d + 1] - base[d]));
+        if (ok) wires = PyList_New(nd);
+        for (Py_ssize_t d = 0; wires && d < nd; ++d) {
+            /* allocated here, filled below without the GIL (not yet shared) */
+            PyObject *o = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)cl[d]);
             if (!o) {
                 Py_CLEAR(wires);
-                goto done;
+                break;
             }
             PyList_SetItem(wires, d, o);
+            cd[d] = (uint8_t *)PyBytes_AsString(o);
+            cs[d] = src + base[d];
         }
-        ret = PyTuple_Pack(2, wires, res);
+        if (wires) {
+            Py_BEGIN_ALLOW_THREADS
+            par_copy(cd, cs, cl, (size_t)nd, total);
+            Py_END_ALLOW_THREADS
+            ret = PyTuple_Pack(2, wires, res);
+        }
+        free(cd), free(cs), free(cl);
     }
 done:
     Py_XDECREF(wires);
@@ -1236,6 +1312,302 @@ done:
     return ret;
 }
 
+/* ------------------------------------------ batched receive, short headers -- */
+
+/* Identity map from object pointers to small indices (open addressing). */
+typedef struct {
+    const void **key;
+    uint32_t *val;
+    size_t cap;
+} PtrMap;
+
+static int ptrmap_init(PtrMap *m, size_t n)
+{
+    m->cap = 16;
+    while (m->cap < 2 * n + 1) m->cap <<= 1;
+    m->key = (const void **)calloc(m->cap, sizeof(void *));
+    m->val = (uint32_t *)calloc(m->cap, sizeof(uint32_t));
+    return m->key && m->val ? 0 : -1;
+}
+
+static void ptrmap_free(PtrMap *m)
+{
+    free(m->key);
+    free(m->val);
+}
+
+/* index of k, or insert it with value v (returns the stored value) */
+static uint32_t ptrmap_get(PtrMap *m, const void *k, uint32_t v, int *inserted)
+{
+    size_t h = ((uintptr_t)k >> 4) * 0x9E3779B97F4A7C15ull;
+    for (size_t i = h & (m->cap - 1);; i = (i + 1) & (m->cap - 1)) {
+        if (m->key[i] == k) {
+            *inserted = 0;
+            return m->val[i];
+        }
+        if (!m->key[i]) {
+            m->key[i] = k;
+            m->val[i] = v;
+            *inserted = 1;
+            return v;
+        }
+    }
+}
+
+/* first_of_each(items) -> the distinct first elements of the (a, b) tuples of
+ * `items`, by identity, in first-seen order (the connections of a batch of
+ * (connection, datagram) pairs). */
+static PyObject *py_first_of_each(PyObject *m, PyObject *args)
+{
+    PyObject *items;
+    if (!PyArg_ParseTuple(args, "O!", &PyList_Type, &items)) return NULL;
+    const Py_ssize_t n = PyList_Size(items);
+    PtrMap pm;
+    if (ptrmap_init(&pm, 64) < 0) return PyErr_NoMemory();
+    PyObject *out = PyList_New(0);
+    for (Py_ssize_t i = 0; out && i < n; ++i) {
+        PyObject *it = PyList_GetItem(items, i);
+        PyObject *a = PyTuple_Check(it) && PyTuple_Size(it) == 2 ? PyTuple_GetItem(it, 0) : NULL;
+        if (!a) {
+            PyErr_SetString(PyExc_TypeError, "items must be (connection, datagram) tuples");
+            Py_CLEAR(out);
+            break;
+        }
+        int ins;
+        if ((size_t)PyList_Size(out) * 2 + 2 > pm.cap) {
+            /* grow: rebuild from the list */
+            PtrMap g;
+            if (ptrmap_init(&g, (size_t)PyList_Size(out) * 2 + 2) < 0) {
+                Py_CLEAR(out);
+                PyErr_NoMemory();
+                break;
+            }
+            for (Py_ssize_t k = 0; k < PyList_Size(out); ++k) (void)ptrmap_get(&g, PyList_GetItem(out, k), (uint32_t)k, &ins);
+            ptrmap_free(&pm);
+            pm = g;
+        }
+        (void)ptrmap_get(&pm, a, (uint32_t)PyList_Size(out), &ins);
+        if (ins && PyList_Append(out, a) < 0) Py_CLEAR(out);
+    }
+    ptrmap_free(&pm);
+    return out;
+}
+
+/* A record of the caller's tuple subclass (receive.ReceivedPacket), built
+ * without a Python-level call: fields are borrowed references. */
+static PyObject *make_record(PyTypeObject *tp, allocfunc alloc, PyObject *const *f, int nf)
+{
+    PyObject *r = alloc(tp, nf);
+    if (!r) return NULL;
+    for (int k = 0; k < nf; ++k) {
+        Py_INCREF(f[k]);
+        if (PyTuple_SetItem(r, k, f[k]) < 0) {
+            Py_DECREF(r);
+            return NULL;
+        }
+    }
+    return r;
+}
+
+/* receive_short(table, items, conns, conn_cid_u32, conn_pair_u32,
+ *               conn_space_u32, pair_slot_u32, space_exp_u64, rec_type,
+ *               packet_type, epoch)
+ *     -> None | (records, deferred, space_exp after)
+ * receive_datagrams' steady state in one call: every datagram of `items`
+ * ((connection, bytes) pairs) is a short-header 1-RTT packet running to the
+ * datagram's end (RFC 9000 sec. 12.2), its encrypted offset 1 + the
+ * connection's CID length.  One launch, then the in-order walk of
+ * CryptoPair.decrypt_packet (quic/crypto.py:184-192) with the expected
+ * packet numbers of connection.py:984-985, as unprotect_walk does, and one
+ * record per datagram:
+ *   (datagram, 0, None, packet_type, epoch, plain_header, payload, pn, None),
+ *   or the drop: "key_unavailable" (pair_slot 0xffffffff: no receive key,
+ *   crypto.py:78-79) / "payload_decrypt_error" (connection.py:936-947).
+ * Deferred datagrams (key-phase flip, or a number that decodes differently
+ * by now -- and every later one of their pair or space) get None and their
+ * index in `deferred`, for the caller's general path.  Returns None at once,
+ * with nothing launched, if any datagram is not such a packet. */
+static PyObject *py_receive_short(PyObject *m, PyObject *args)
+{
+    PyObject *t, *items, *conns, *rec_type, *ptype, *epoch;
+    const char *a_cid, *a_pair, *a_space, *a_pslot, *a_sexp;
+    Py_ssize_t l_cid, l_pair, l_space, l_pslot, l_sexp;
+    if (!PyArg_ParseTuple(args, "OO!O!y#y#y#y#y#OOO", &t, &PyList_Type, &items, &PyList_Type, &conns, &a_cid, &l_cid,
+                          &a_pair, &l_pair, &a_space, &l_space, &a_pslot, &l_pslot, &a_sexp, &l_sexp, &rec_type,
+                          &ptype, &epoch))
+        return NULL;
+    qpp_keytab *kt = as_table(t);
+    if (!kt) return NULL;
+    if (!PyType_Check(rec_type) || !PyType_IsSubtype((PyTypeObject *)rec_type, &PyTuple_Type)) {
+        PyErr_SetString(PyExc_TypeError, "rec_type must be a tuple subclass");
+        return NULL;
+    }
+    const Py_ssize_t n = PyList_Size(items), nc = PyList_Size(conns);
+    const Py_ssize_t n_pairs = l_pslot / 4, n_spaces = l_sexp / 8;
+    if (check_len(l_cid, nc, 4, "conn_cid") < 0 || check_len(l_pair, nc, 4, "conn_pair") < 0 ||
+        check_len(l_space, nc, 4, "conn_space") < 0)
+        return NULL;
+    const uint32_t *ccid = (const uint32_t *)a_cid, *cpair = (const uint32_t *)a_pair,
+                   *cspace = (const uint32_t *)a_space, *pslot = (const uint32_t *)a_pslot;
+    for (Py_ssize_t c = 0; c < nc; ++c)
+        if ((Py_ssize_t)cpair[c] >= n_pairs || (Py_ssize_t)cspace[c] >= n_spaces) {
+            PyErr_SetString(PyExc_ValueError, "pair or space index out of range");
+            return NULL;
+        }
+    PyTypeObject *tp = (PyTypeObject *)rec_type;
+    allocfunc alloc = (allocfunc)PyType_GetSlot(tp, Py_tp_alloc);
+    if (!alloc) return NULL;
+
+    PtrMap pm = {0};
+    uint32_t *conn_of = NULL, *slot_of = NULL;
+    qpp_desc *desc = NULL;
+    uint8_t **cd = NULL;
+    const uint8_t **cs = NULL;
+    size_t *cl = NULL;
+    uint8_t *blocked_pair = NULL, *blocked_space = NULL;
+    PyObject *ret = NULL, *recs = NULL, *res = NULL, *deferred = NULL, *sexp_out = NULL;
+    PyObject *empty = NULL, *minus1 = NULL, *s_key = NULL, *s_dec = NULL;
+    int ins;
+    if (ptrmap_init(&pm, (size_t)nc) < 0) goto nomem;
+    for (Py_ssize_t c = 0; c < nc; ++c) (void)ptrmap_get(&pm, PyList_GetItem(conns, c), (uint32_t)c, &ins);
+    conn_of = (uint32_t *)malloc((n ? (size_t)n : 1) * sizeof(uint32_t));
+    slot_of = (uint32_t *)malloc((n ? (size_t)n : 1) * sizeof(uint32_t));
+    desc = (qpp_desc *)calloc(n ? (size_t)n : 1, sizeof(qpp_desc));
+    cd = (uint8_t **)malloc((n ? (size_t)n : 1) * sizeof(uint8_t *));
+    cs = (const uint8_t **)malloc((n ? (size_t)n : 1) * sizeof(uint8_t *));
+    cl = (size_t *)malloc((n ? (size_t)n : 1) * sizeof(size_t));
+    blocked_pair = (uint8_t *)calloc(n_pairs ? (size_t)n_pairs : 1, 1);
+    blocked_space = (uint8_t *)calloc(n_spaces ? (size_t)n_spaces : 1, 1);
+    if (!conn_of || !slot_of || !desc || !cd || !cs || !cl || !blocked_pair || !blocked_space) goto nomem;
+    /* classify: every datagram a short header long enough for its CID */
+    size_t total = 0;
+    uint32_t nl = 0;  /* packets to launch */
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject *it = PyList_GetItem(items, i);
+        PyObject *c = PyTuple_Check(it) && PyTuple_Size(it) == 2 ? PyTuple_GetItem(it, 0) : NULL;
+        PyObject *d = c ? PyTuple_GetItem(it, 1) : NULL;
+        if (!d || !PyBytes_Check(d)) goto fallback;
+        const int found = (int)ptrmap_get(&pm, c, 0xffffffffu, &ins);
+        if (ins) goto fallback; /* a connection not in conns */
+        const Py_ssize_t len = PyBytes_Size(d);
+        const uint8_t *b = (const uint8_t *)PyBytes_AsString(d);
+        if (len < 1 || (b[0] & 0xC0) != 0x40 || len < 1 + (Py_ssize_t)ccid[found]) goto fallback;
+        conn_of[i] = (uint32_t)found;
+        slot_of[i] = pslot[cpair[found]];
+        if (slot_of[i] == 0xffffffffu) continue; /* no receive key: no launch */
+        qpp_desc *x = &desc[nl];
+        x->in_off = x->out_off = total;
+        x->len = (uint32_t)len;
+        x->hdr_len = (uint16_t)(1 + ccid[found]);
+        x->pn = ((const uint64_t *)a_sexp)[cspace[found]];
+        x->slot = slot_of[i];
+        x->rsv = (uint32_t)i; /* the datagram (host-side bookkeeping only) */
+        cs[nl] = b;
+        cl[nl] = (size_t)len;
+        total += (size_t)len;
+        ++nl;
+    }
+    res = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)nl * (Py_ssize_t)sizeof(qpp_result));
+    sexp_out = PyBytes_FromStringAndSize(a_sexp, l_sexp);
+    recs = PyList_New(n);
+    deferred = PyList_New(0);
+    empty = PyBytes_FromStringAndSize("", 0);
+    minus1 = PyLong_FromLong(-1);
+    s_key = PyUnicode_FromString("key_unavailable");
+    s_dec = PyUnicode_FromString("payload_decrypt_error");
+    if (!res || !sexp_out || !recs || !deferred || !empty || !minus1 || !s_key || !s_dec) goto nomem;
+    uint8_t *hin = NULL, *hout = NULL;
+    if (nl) {
+        qpp_session *ss = session();
+        if (!ss || check_rc(qpp_session_stage(ss, total ? total : 1, nl, &hin, &hout)) < 0) goto done;
+        for (uint32_t k = 0; k < nl; ++k) cd[k] = hin + desc[k].in_off;
+        Py_BEGIN_ALLOW_THREADS  /* `items` holds every datagram */
+        par_copy(cd, cs, cl, nl, total);
+        Py_END_ALLOW_THREADS
+        if (host_call(0, kt, desc, nl, hin, total, hout, total, PyBytes_AsString(res)) < 0) goto done;
+    }
+    {
+        uint64_t *sx = (uint64_t *)PyBytes_AsString(sexp_out);
+        const qpp_result *r = (const qpp_result *)PyBytes_AsString(res);
+        uint32_t k = 0;
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            PyObject *di = PyLong_FromSsize_t(i);
+            if (!di) goto done;
+            const uint32_t c = conn_of[i], p = cpair[c], sp = cspace[c];
+            PyObject *rec = NULL;
+            if (slot_of[i] == 0xffffffffu) {
+                PyObject *f[9] = {di, PyLong_FromLong(0), Py_None, ptype, epoch, empty, empty, minus1, s_key};
+                if (f[1]) rec = make_record(tp, alloc, f, 9);
+                Py_XDECREF(f[1]);
+            } else {
+                const qpp_result *ri = &r[k];
+                const qpp_desc *dk = &desc[k];
+                ++k;
+                const uint64_t now = sx[sp];
+                int defer = blocked_pair[p] || blocked_space[sp] || ri->status == QPP_S_KEY_PHASE;
+                if (!defer && now != dk->pn && (ri->status == QPP_S_OK || ri->status == QPP_S_DECRYPT)) {
+                    const int pn_len = (int)ri->hdr_len - (int)dk->hdr_len;
+                    if (pn_len < 1 || pn_len > 4 || decode_pn_signed(ri->pn, pn_len, now) != (int64_t)ri->pn)
+                        defer = 1;
+                }
+                if (defer) {
+                    blocked_pair[p] = blocked_space[sp] = 1;
+                    const int bad = PyList_Append(deferred, di);
+                    Py_INCREF(Py_None);
+                    PyList_SetItem(recs, i, Py_None);
+                    Py_DECREF(di);
+                    if (bad < 0) goto done;
+                    continue;
+                }
+                PyObject *zero = PyLong_FromLong(0);
+                if (ri->status == QPP_S_OK) {
+                    const uint8_t *o = hout + dk->out_off;
+                    PyObject *h = PyBytes_FromStringAndSize((const char *)o, ri->hdr_len);
+                    PyObject *pl = PyBytes_FromStringAndSize((const char *)o + ri->hdr_len,
+                                                             (Py_ssize_t)ri->out_len - ri->hdr_len);
+                    PyObject *pn = PyLong_FromUnsignedLongLong(ri->pn);
+                    if (zero && h && pl && pn) {
+                        PyObject *f[9] = {di, zero, Py_None, ptype, epoch, h, pl, pn, Py_None};
+                        rec = make_record(tp, alloc, f, 9);
+                    }
+                    Py_XDECREF(h);
+                    Py_XDECREF(pl);
+                    Py_XDECREF(pn);
+                    if (ri->pn > now) sx[sp] = ri->pn + 1;
+                } else if (zero) {
+                    PyObject *f[9] = {di, zero, Py_None, ptype, epoch, empty, empty, minus1,
+                                      ri->status == QPP_S_NO_KEY ? s_key : s_dec};
+                    rec = make_record(tp, alloc, f, 9);
+                }
+                Py_XDECREF(zero);
+            }
+            Py_DECREF(di);
+            if (!rec) goto done;
+            PyList_SetItem(recs, i, rec);
+        }
+    }
+    ret = PyTuple_Pack(3, recs, deferred, sexp_out);
+    goto done;
+fallback:
+    Py_INCREF(Py_None);
+    ret = Py_None;
+    goto done;
+nomem:
+    PyErr_NoMemory();
+done:
+    ptrmap_free(&pm);
+    free(conn_of), free(slot_of), free(desc), free(cd), free(cs), free(cl), free(blocked_pair), free(blocked_space);
+    Py_XDECREF(recs);
+    Py_XDECREF(res);
+    Py_XDECREF(deferred);
+    Py_XDECREF(sexp_out);
+    Py_XDECREF(empty);
+    Py_XDECREF(minus1);
+    Py_XDECREF(s_key);
+    Py_XDECREF(s_dec);
+    return ret;
+}
+
 static PyObject *py_hp_mask_host(PyObject *m, PyObject *args)
 {
     PyObject *t;
@@ -1290,6 +1662,10 @@ static PyMethodDef module_methods[] = {
     {"unprotect_walk", py_unprotect_walk, METH_VARARGS,
      "unprotect_walk(table, slots_u32, exp_u64, packets, offs_u32, pair_u32, space_u32, track_u8, space_exp_u64, "
      "n_pairs) -> (outcomes, results, deferred)"},
+    {"first_of_each", py_first_of_each, METH_VARARGS, "first_of_each(items) -> distinct first elements, by identity"},
+    {"receive_short", py_receive_short, METH_VARARGS,
+     "receive_short(table, items, conns, conn_cid_u32, conn_pair_u32, conn_space_u32, pair_slot_u32, space_exp_u64, "
+     "rec_type, packet_type, epoch) -> None | (records, deferred, space_exp)"},
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},

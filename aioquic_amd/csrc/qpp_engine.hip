@@ -2409,7 +2409,7 @@ static int multi_run(bool enc, qpp_multi *m, const qpp_desc *desc, uint32_t n, c
     }
     int parts = m->n < (int)n ? m->n : (int)n;
     // bounds first (as a session does), so that extents use only packets
-    // that fit; rejected ones keep offset 0 in their range and touch nothing
+    // that fit; rejected ones stay rejected in their range and touch nothing
     std::vector<qpp_desc> d(desc, desc + n);
     reject_out_of_bounds(enc, d.data(), n, in_len, out_len);
     struct Range {
@@ -2454,7 +2454,8 @@ static int multi_run(bool enc, qpp_multi *m, const qpp_desc *desc, uint32_t n, c
     for (int k = 0; k < parts; ++k)
         for (uint32_t i = r[k].b; i < r[k].e; ++i) {
             if (d[i].flags & kFlagReject) {
-                d[i].in_off = d[i].out_off = 0;
+                // past every range buffer: the range's session rejects it again
+                d[i].in_off = d[i].out_off = ~0ull;
                 continue;
             }
             d[i].in_off -= r[k].ilo;

@@ -22,7 +22,6 @@ reference's.
 
 from __future__ import annotations
 
-import threading
 from dataclasses import dataclass, field
 from enum import Enum
 from typing import Any, Callable, Optional, Sequence
@@ -31,7 +30,7 @@ import numpy as np
 
 from . import layout as L
 from ._crypto import protect_datagrams
-from .batch_io import KeySlots, _raise_status
+from .batch_io import KeySlots, _raise_status, default_slots
 from .buffer import Buffer, size_uint_var
 from .tls import Epoch
 from .packet import (
@@ -121,17 +120,8 @@ class _Pending:
         return zip(self.dg, self.off, self.hsize, self.size, self.pn, (self.keys[r] for r in self.ref))
 
 
-_per_thread = threading.local()
-
-
 def _default_slots() -> KeySlots:
-    """The builders' default key table: one per OS thread, so concurrent
-    flushes on different threads never assign or reset each other's slots
-    (the C extension gives each thread its own staging the same way)."""
-    t = getattr(_per_thread, "slots", None)
-    if t is None:
-        t = _per_thread.slots = KeySlots(4096)
-    return t
+    return default_slots()
 
 
 class QuicPacketBuilder:

@@ -25,8 +25,9 @@ from typing import Any, Dict, List, NamedTuple, Optional, Sequence, Tuple
 
 import numpy as np
 
+from . import _crypto
 from ._crypto import CryptoError
-from .batch_io import ReceiveBatch
+from .batch_io import ReceiveBatch, default_slots
 from .buffer import Buffer
 from .crypto import KeyUnavailableError
 from .packet import (
@@ -135,6 +136,61 @@ def _walk_long(conn: ConnectionKeys, d: int, data: bytes, out: list, queued: lis
         add(pair, data[start:end], enc_off, space)
 
 
+def _receive_short(items: list) -> Optional[List[ReceivedPacket]]:
+    """The steady state in C (_crypto.receive_short): every datagram one
+    short-header packet.  None (nothing launched) when any is not; the
+    caller then walks the batch in Python."""
+    conns = _crypto.first_of_each(items)
+    pix: dict = {}
+    six: dict = {}
+    upairs, uspaces, c_pair, c_space, c_cid = [], [], [], [], []
+    for conn in conns:
+        pair, space = conn.pair_and_space(Epoch.ONE_RTT, None)
+        if id(pair) not in pix:
+            pix[id(pair)] = len(upairs)
+            upairs.append(pair)
+        if id(space) not in six:
+            six[id(space)] = len(uspaces)
+            uspaces.append(space)
+        c_pair.append(pix[id(pair)])
+        c_space.append(six[id(space)])
+        c_cid.append(conn.host_cid_length)
+    slots = default_slots()
+    keyed = [k for k, p in enumerate(upairs) if p.recv.aead is not None]
+    pslot = np.full(len(upairs), 0xFFFFFFFF, np.uint32)
+    if keyed:
+        rc = [upairs[k].recv for k in keyed]
+        pslot[keyed] = slots.assign([(c.aead, c.hp, c.key_phase) for c in rc])
+    sexp = np.asarray([sp.expected_packet_number & 0xFFFFFFFFFFFFFFFF for sp in uspaces], np.uint64)
+    got = _crypto.receive_short(slots.table, items, conns, np.asarray(c_cid, np.uint32).tobytes(),
+                                np.asarray(c_pair, np.uint32).tobytes(), np.asarray(c_space, np.uint32).tobytes(),
+                                pslot.tobytes(), sexp.tobytes(), ReceivedPacket, QuicPacketType.ONE_RTT,
+                                Epoch.ONE_RTT)
+    if got is None:
+        return None
+    recs, deferred, sexp2 = got
+    new = np.frombuffer(sexp2, dtype=np.uint64)
+    for k in np.flatnonzero(new != sexp).tolist():
+        uspaces[k].expected_packet_number = int(new[k])
+    if deferred:
+        # key-phase flips and numbers decoded under a stale expected number:
+        # the general walk takes them in order from the state left above
+        rb = ReceiveBatch(slots=slots)
+        for d in deferred:
+            conn, data = items[d]
+            pair, space = conn.pair_and_space(Epoch.ONE_RTT, None)
+            rb.add(pair, data, 1 + conn.host_cid_length, space=space)
+        for d, res in zip(deferred, rb.run()):
+            f = (d, 0, None, QuicPacketType.ONE_RTT, Epoch.ONE_RTT)
+            if isinstance(res, tuple):
+                recs[d] = _new(ReceivedPacket, f + res + (None,))
+            elif isinstance(res, KeyUnavailableError):
+                recs[d] = _new(ReceivedPacket, f + (b"", b"", -1, "key_unavailable"))
+            else:
+                recs[d] = _new(ReceivedPacket, f + (b"", b"", -1, "payload_decrypt_error"))
+    return recs
+
+
 def receive_datagrams(items: Sequence[Tuple[ConnectionKeys, bytes]],
                       batch: Optional[ReceiveBatch] = None) -> List[ReceivedPacket]:
     """Parse and unprotect every packet of every (connection, datagram) in
@@ -146,9 +202,13 @@ def receive_datagrams(items: Sequence[Tuple[ConnectionKeys, bytes]],
     end of the datagram.  Every packet goes into one ReceiveBatch, whose first
     round (one launch and the in-order walk) runs in C."""
     own = batch is None
-    batch = batch or ReceiveBatch()
     if not items:
         return []
+    if own:
+        fast = _receive_short(items if isinstance(items, list) else list(items))
+        if fast is not None:
+            return fast
+    batch = batch or ReceiveBatch(slots=default_slots())
     first = np.fromiter((dg[0] if dg else 0 for _, dg in items), np.uint8, len(items))
     short = ((first & (PACKET_LONG_HEADER | PACKET_FIXED_BIT)) == PACKET_FIXED_BIT).tolist()
     out: list = []

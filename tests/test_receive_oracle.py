@@ -276,3 +276,29 @@ def test_receive_batch_corrupt_packets_bounded_launches():
             assert not isinstance(g, tuple)
     assert sum(isinstance(g, tuple) for g in got) == 160
     assert batch.launches <= 3, batch.launches  # the batch, the key-phase retry, one check
+
+
+@pytest.mark.gpu
+def test_receive_datagrams_short_only_vs_oracle_walk(monkeypatch):
+    """The steady state (every datagram one short-header packet) takes the C
+    path (_crypto.receive_short); its deferrals (key-phase flip, stale
+    decodes) continue in the general walk.  Outcomes and state equal the
+    oracle walk's."""
+    from aioquic_amd import _crypto
+    from aioquic_amd import receive as R
+    from aioquic_amd.tls import Epoch
+
+    specs, items = RS.build(seed=0x5A, n_conns=7, per_conn=90)
+    items = [(c, d) for c, d in items if d and (d[0] & 0xC0) == 0x40 and len(d) >= 9]
+    calls = []
+    real = _crypto.receive_short
+    monkeypatch.setattr(_crypto, "receive_short", lambda *a: calls.append(1) or real(*a))
+    oconns = [s.oracle_conn() for s in specs]
+    pconns = [s.product_conn() for s in specs]
+    want = W.receive([(oconns[c], d) for c, d in items])
+    got = R.receive_datagrams([(pconns[c], d) for c, d in items])
+    assert calls == [1]
+    assert [_product_tuple(g) for g in got] == [_oracle_tuple(w) for w in want]
+    assert {"payload_decrypt_error", "key_unavailable", None} <= {w.dropped for w in want}
+    for oc, pc in zip(oconns, pconns):
+        assert oc.expected["ONE_RTT"] == pc.spaces[Epoch.ONE_RTT].expected_packet_number
