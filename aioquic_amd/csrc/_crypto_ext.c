@@ -1466,7 +1466,10 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     size_t *cl = NULL;
     uint8_t *blocked_pair = NULL, *blocked_space = NULL;
     PyObject *ret = NULL, *recs = NULL, *res = NULL, *deferred = NULL, *sexp_out = NULL;
-    PyObject *empty = NULL, *minus1 = NULL, *s_key = NULL, *s_dec = NULL;
+    PyObject *empty = NULL, *minus1 = NULL, *zero = NULL, *s_key = NULL, *s_dec = NULL;
+    uint8_t **od = NULL;
+    const uint8_t **os_ = NULL;
+    size_t *ol = NULL, on = 0, otot = 0;
     int ins;
     if (ptrmap_init(&pm, (size_t)nc) < 0) goto nomem;
     for (Py_ssize_t c = 0; c < nc; ++c) (void)ptrmap_get(&pm, PyList_GetItem(conns, c), (uint32_t)c, &ins);
@@ -1478,7 +1481,13 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     cl = (size_t *)malloc((n ? (size_t)n : 1) * sizeof(size_t));
     blocked_pair = (uint8_t *)calloc(n_pairs ? (size_t)n_pairs : 1, 1);
     blocked_space = (uint8_t *)calloc(n_spaces ? (size_t)n_spaces : 1, 1);
-    if (!conn_of || !slot_of || !desc || !cd || !cs || !cl || !blocked_pair || !blocked_space) goto nomem;
+    /* output copies: header and payload of every packet, filled after the
+       walk without the GIL (the bytes objects are not shared until returned) */
+    od = (uint8_t **)malloc((2 * (size_t)n + 1) * sizeof(uint8_t *));
+    os_ = (const uint8_t **)malloc((2 * (size_t)n + 1) * sizeof(uint8_t *));
+    ol = (size_t *)malloc((2 * (size_t)n + 1) * sizeof(size_t));
+    if (!conn_of || !slot_of || !desc || !cd || !cs || !cl || !blocked_pair || !blocked_space || !od || !os_ || !ol)
+        goto nomem;
     /* classify: every datagram a short header long enough for its CID */
     size_t total = 0;
     uint32_t nl = 0;  /* packets to launch */
@@ -1513,9 +1522,10 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     deferred = PyList_New(0);
     empty = PyBytes_FromStringAndSize("", 0);
     minus1 = PyLong_FromLong(-1);
+    zero = PyLong_FromLong(0);
     s_key = PyUnicode_FromString("key_unavailable");
     s_dec = PyUnicode_FromString("payload_decrypt_error");
-    if (!res || !sexp_out || !recs || !deferred || !empty || !minus1 || !s_key || !s_dec) goto nomem;
+    if (!res || !sexp_out || !recs || !deferred || !empty || !minus1 || !zero || !s_key || !s_dec) goto nomem;
     uint8_t *hin = NULL, *hout = NULL;
     if (nl) {
         qpp_session *ss = session();
@@ -1536,9 +1546,8 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
             const uint32_t c = conn_of[i], p = cpair[c], sp = cspace[c];
             PyObject *rec = NULL;
             if (slot_of[i] == 0xffffffffu) {
-                PyObject *f[9] = {di, PyLong_FromLong(0), Py_None, ptype, epoch, empty, empty, minus1, s_key};
-                if (f[1]) rec = make_record(tp, alloc, f, 9);
-                Py_XDECREF(f[1]);
+                PyObject *f[9] = {di, zero, Py_None, ptype, epoch, empty, empty, minus1, s_key};
+                rec = make_record(tp, alloc, f, 9);
             } else {
                 const qpp_result *ri = &r[k];
                 const qpp_desc *dk = &desc[k];
@@ -1559,14 +1568,16 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
                     if (bad < 0) goto done;
                     continue;
                 }
-                PyObject *zero = PyLong_FromLong(0);
                 if (ri->status == QPP_S_OK) {
                     const uint8_t *o = hout + dk->out_off;
-                    PyObject *h = PyBytes_FromStringAndSize((const char *)o, ri->hdr_len);
-                    PyObject *pl = PyBytes_FromStringAndSize((const char *)o + ri->hdr_len,
-                                                             (Py_ssize_t)ri->out_len - ri->hdr_len);
+                    const size_t pll = (size_t)ri->out_len - ri->hdr_len;
+                    PyObject *h = PyBytes_FromStringAndSize(NULL, ri->hdr_len);
+                    PyObject *pl = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)pll);
                     PyObject *pn = PyLong_FromUnsignedLongLong(ri->pn);
-                    if (zero && h && pl && pn) {
+                    if (h && pl && pn) {
+                        od[on] = (uint8_t *)PyBytes_AsString(h), os_[on] = o, ol[on++] = ri->hdr_len;
+                        od[on] = (uint8_t *)PyBytes_AsString(pl), os_[on] = o + ri->hdr_len, ol[on++] = pll;
+                        otot += ri->hdr_len + pll;
                         PyObject *f[9] = {di, zero, Py_None, ptype, epoch, h, pl, pn, Py_None};
                         rec = make_record(tp, alloc, f, 9);
                     }
@@ -1574,18 +1585,20 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
                     Py_XDECREF(pl);
                     Py_XDECREF(pn);
                     if (ri->pn > now) sx[sp] = ri->pn + 1;
-                } else if (zero) {
+                } else {
                     PyObject *f[9] = {di, zero, Py_None, ptype, epoch, empty, empty, minus1,
                                       ri->status == QPP_S_NO_KEY ? s_key : s_dec};
                     rec = make_record(tp, alloc, f, 9);
                 }
-                Py_XDECREF(zero);
             }
             Py_DECREF(di);
             if (!rec) goto done;
             PyList_SetItem(recs, i, rec);
         }
     }
+    Py_BEGIN_ALLOW_THREADS
+    par_copy(od, os_, ol, on, otot);
+    Py_END_ALLOW_THREADS
     ret = PyTuple_Pack(3, recs, deferred, sexp_out);
     goto done;
 fallback:
@@ -1597,6 +1610,8 @@ nomem:
 done:
     ptrmap_free(&pm);
     free(conn_of), free(slot_of), free(desc), free(cd), free(cs), free(cl), free(blocked_pair), free(blocked_space);
+    free(od), free(os_), free(ol);
+    Py_XDECREF(zero);
     Py_XDECREF(recs);
     Py_XDECREF(res);
     Py_XDECREF(deferred);

@@ -22,6 +22,7 @@ reference's.
 
 from __future__ import annotations
 
+from array import array
 from dataclasses import dataclass, field
 from enum import Enum
 from typing import Any, Callable, Optional, Sequence
@@ -90,12 +91,13 @@ class _Pending:
     __slots__ = ("dg", "off", "hsize", "size", "pn", "ref", "keys", "_key_ix")
 
     def __init__(self) -> None:
-        self.dg: list = []
-        self.off: list = []
-        self.hsize: list = []
-        self.size: list = []
-        self.pn: list = []
-        self.ref: list = []
+        # typed arrays: appended per packet, handed to numpy without a copy
+        self.dg = array("I")
+        self.off = array("I")
+        self.hsize = array("I")
+        self.size = array("I")
+        self.pn = array("Q")
+        self.ref = array("I")
         self.keys: list = []
         self._key_ix: dict = {}
 
@@ -374,12 +376,12 @@ def _protect_datagrams(plains: list, pending: list, slots: Optional[KeySlots]) -
     base = 0
     for (count, pend), first in zip(pending, firsts):
         if len(pend):
-            cols["dg"].append(np.asarray(pend.dg, np.uint32) + np.uint32(base))
-            cols["off"].append(np.asarray(pend.off, np.uint32))
-            cols["hsize"].append(np.asarray(pend.hsize, np.uint32))
-            cols["size"].append(np.asarray(pend.size, np.uint32))
-            cols["pn"].append(np.asarray(pend.pn, np.uint64))
-            cols["slot"].append(per_key[first + np.asarray(pend.ref, np.int64)])
+            cols["dg"].append(np.frombuffer(pend.dg, np.uint32) + np.uint32(base))
+            cols["off"].append(np.frombuffer(pend.off, np.uint32))
+            cols["hsize"].append(np.frombuffer(pend.hsize, np.uint32))
+            cols["size"].append(np.frombuffer(pend.size, np.uint32))
+            cols["pn"].append(np.frombuffer(pend.pn, np.uint64))
+            cols["slot"].append(per_key[first + np.frombuffer(pend.ref, np.uint32)])
         base += count
     arr = {k: (np.concatenate(v) if v else np.zeros(0, np.uint64 if k == "pn" else np.uint32)).tobytes()
            for k, v in cols.items()}

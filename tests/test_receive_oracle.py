@@ -275,7 +275,9 @@ def test_receive_batch_corrupt_packets_bounded_launches():
         except W.DecryptError:
             assert not isinstance(g, tuple)
     assert sum(isinstance(g, tuple) for g in got) == 160
-    assert batch.launches <= 3, batch.launches  # the batch, the key-phase retry, one check
+    # the C round, then one general round for what it deferred: the batch, the
+    # key-phase retry and one confirming launch -- not one launch per corrupt packet
+    assert batch.launches <= 4, batch.launches
 
 
 @pytest.mark.gpu
