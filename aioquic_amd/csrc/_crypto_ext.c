@@ -1002,6 +1002,7 @@ static PyObject *batch_list(PyObject *args, int enc)
                 item = (h && p) ? PyTuple_Pack(2, h, p) : NULL;
                 Py_XDECREF(h);
                 Py_XDECREF(p);
+                if (item) PyObject_GC_UnTrack(item); /* two bytes objects: never in a cycle */
             } else {
                 Py_INCREF(Py_None);
                 item = Py_None;
@@ -1296,6 +1297,7 @@ static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
             Py_XDECREF(pl);
             Py_XDECREF(pn);
             if (!item) goto done;
+            PyObject_GC_UnTrack(item); /* bytes and an int: never in a cycle (make_record) */
             PyList_SetItem(outs, i, item);
             if (track[i] && r[i].pn > now) sx[sp] = r[i].pn + 1;
         }
@@ -1394,7 +1396,11 @@ static PyObject *py_first_of_each(PyObject *m, PyObject *args)
 }
 
 /* A record of the caller's tuple subclass (receive.ReceivedPacket), built
- * without a Python-level call: fields are borrowed references. */
+ * without a Python-level call: fields are borrowed references.  A record
+ * refers only to objects that cannot refer back to it (ints, bytes, None,
+ * enum members), so it can never be part of a reference cycle: it is taken
+ * off the cycle collector's lists, which a batch of 64 Ki records would
+ * otherwise keep traversing. */
 static PyObject *make_record(PyTypeObject *tp, allocfunc alloc, PyObject *const *f, int nf)
 {
     PyObject *r = alloc(tp, nf);
@@ -1406,6 +1412,7 @@ static PyObject *make_record(PyTypeObject *tp, allocfunc alloc, PyObject *const 
             return NULL;
         }
     }
+    PyObject_GC_UnTrack(r);
     return r;
 }
 
