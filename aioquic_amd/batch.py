@@ -173,6 +173,25 @@ class MultiDeviceEngine:
         out, res = self.multi.unprotect(np.ascontiguousarray(desc).tobytes(), bytes(data), int(out_len))
         return np.frombuffer(out, dtype=np.uint8), np.frombuffer(res, dtype=L.RESULT)
 
+    def protect_into(self, desc: np.ndarray, data: np.ndarray, out: np.ndarray, results: np.ndarray) -> None:
+        """protect_host into caller-owned arrays, reusable across batches."""
+        _into_arrays(self.multi.protect_into, desc, data, out, results)
+
+    def unprotect_into(self, desc: np.ndarray, data: np.ndarray, out: np.ndarray, results: np.ndarray) -> None:
+        _into_arrays(self.multi.unprotect_into, desc, data, out, results)
+
+
+def _into_arrays(fn, desc, data, out, results) -> None:
+    desc = np.ascontiguousarray(desc, dtype=L.DESC)
+    data = np.ascontiguousarray(data).view(np.uint8).ravel()
+    if not (out.flags.c_contiguous and out.flags.writeable):
+        raise ValueError("out must be a writable contiguous array")
+    if not (results.flags.c_contiguous and results.flags.writeable) or \
+            results.nbytes < len(desc) * L.RESULT.itemsize:
+        raise ValueError("results must be a writable contiguous array of len(desc) records")
+    fn(desc.ctypes.data, len(desc), data.ctypes.data, data.nbytes, out.ctypes.data, out.nbytes,
+       results.ctypes.data)
+
 
 def layout_packets(headers, payloads, pns, slots, *, align: int = 1, tag_room: bool = True,
                    flags: int = 0, payload_align: int = 1):

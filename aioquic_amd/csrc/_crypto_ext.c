@@ -737,6 +737,31 @@ static PyObject *multi_run_py(MultiObject *self, PyObject *args, int enc)
 static PyObject *Multi_protect(MultiObject *self, PyObject *args) { return multi_run_py(self, args, 1); }
 static PyObject *Multi_unprotect(MultiObject *self, PyObject *args) { return multi_run_py(self, args, 0); }
 
+/* protect_into / unprotect_into(desc_ptr, n, in_ptr, in_len, out_ptr, out_len,
+ * res_ptr): host memory by address (caller-owned, reused across batches). */
+static PyObject *multi_into_py(MultiObject *self, PyObject *args, int enc)
+{
+    unsigned long long dp, ip, op, rp, in_len, out_len;
+    unsigned int n;
+    if (!PyArg_ParseTuple(args, "KIKKKKK", &dp, &n, &ip, &in_len, &op, &out_len, &rp)) return NULL;
+    if (n && (!dp || !rp || (in_len && !ip) || (out_len && !op))) {
+        PyErr_SetString(PyExc_ValueError, "null buffer");
+        return NULL;
+    }
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = enc ? qpp_multi_protect(self->m, (const qpp_desc *)as_ptr(dp), n, (const uint8_t *)as_ptr(ip),
+                                 (size_t)in_len, (uint8_t *)as_ptr(op), (size_t)out_len, (qpp_result *)as_ptr(rp))
+             : qpp_multi_unprotect(self->m, (const qpp_desc *)as_ptr(dp), n, (const uint8_t *)as_ptr(ip),
+                                   (size_t)in_len, (uint8_t *)as_ptr(op), (size_t)out_len, (qpp_result *)as_ptr(rp));
+    Py_END_ALLOW_THREADS
+    if (check_rc(rc) < 0) return NULL;
+    Py_RETURN_NONE;
+}
+
+static PyObject *Multi_protect_into(MultiObject *self, PyObject *args) { return multi_into_py(self, args, 1); }
+static PyObject *Multi_unprotect_into(MultiObject *self, PyObject *args) { return multi_into_py(self, args, 0); }
+
 static PyObject *Multi_devices(MultiObject *self, void *unused)
 {
     return PyLong_FromLong(qpp_multi_devices(self->m));
@@ -746,6 +771,10 @@ static PyMethodDef Multi_methods[] = {
     {"set_keys", (PyCFunction)Multi_set_keys, METH_VARARGS, "set_keys(materials) on every device"},
     {"protect", (PyCFunction)Multi_protect, METH_VARARGS, "protect(desc, data, out_len) -> (out, results)"},
     {"unprotect", (PyCFunction)Multi_unprotect, METH_VARARGS, "unprotect(desc, data, out_len) -> (out, results)"},
+    {"protect_into", (PyCFunction)Multi_protect_into, METH_VARARGS,
+     "protect_into(desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
+    {"unprotect_into", (PyCFunction)Multi_unprotect_into, METH_VARARGS,
+     "unprotect_into(desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
     {NULL},
 };
 

@@ -579,6 +579,12 @@ def _workload_name(cfg, n):
     return cfg["name"].replace(ki(cfg["n"]), ki(n), 1)
 
 
+def L_RESULT():
+    from aioquic_amd import layout as L
+
+    return L.RESULT
+
+
 def e2e_host_devices(cfg, seed, n, reps=3):
     """The library's own host-buffer path over every visible GPU
     (MultiDeviceEngine / qpp_multi: one host batch cut into contiguous ranges,
@@ -592,21 +598,27 @@ def e2e_host_devices(cfg, seed, n, reps=3):
     w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=seed, version=cfg["version"],
                       mixed=cfg.get("mixed"))
     out = {}
+    wire = np.empty(w.wire_size, np.uint8)
+    back = np.empty(w.plain_size, np.uint8)
+    r1 = np.empty(n, L_RESULT())
+    r2 = np.empty(n, L_RESULT())
     for d in range(1, torch.cuda.device_count() + 1):
         eng = MultiDeviceEngine(w.n_keys, devices=list(range(d)))
         eng.set_key_records(w.keys)
-        wire, _ = eng.protect_host(w.desc, w.plain, w.wire_size)  # warm-up (staging allocation)
+        eng.protect_into(w.desc, w.plain, wire, r1)  # warm-up (staging allocation, first touch)
+        eng.unprotect_into(w.udesc, wire, back, r2)
         times = []
         for _ in range(reps):
             t0 = time.perf_counter()
-            wire, r1 = eng.protect_host(w.desc, w.plain, w.wire_size)
-            back, r2 = eng.unprotect_host(w.udesc, wire, w.plain_size)
+            eng.protect_into(w.desc, w.plain, wire, r1)
+            eng.unprotect_into(w.udesc, wire, back, r2)
             times.append(time.perf_counter() - t0)
         ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all() and np.array_equal(back, w.plain))
         out[str(d)] = {"gib_s": round(n * 1200 / float(np.median(times)) / GIB, 3), "round_trip_ok": ok}
         del eng
     return {"per_device_count": out, "packets": n,
-            "note": "host bytes -> qpp_multi protect -> host, host -> unprotect -> host (two synchronous calls)"}
+            "note": "caller-owned host arrays: qpp_multi protect_into, then unprotect_into (two synchronous "
+                    "calls, each staged through pinned memory, H2D, kernel, D2H)"}
 
 
 def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5, mode="staged"):

@@ -62,3 +62,23 @@ def test_multi_rejects_and_overlap_like_one_session():
     a = one.protect_host(rev, w.plain, w.wire_size)
     b = multi.protect_host(rev, w.plain, w.wire_size)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_multi_into_caller_buffers():
+    """The caller-owned-buffer form (the bench's host path) writes the same
+    bytes and results as the bytes-returning form."""
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import MultiDeviceEngine
+
+    w = _workload(2048, 0x53)
+    multi = MultiDeviceEngine(w.n_keys, devices=[0, 0])
+    multi.set_key_records(w.keys)
+    wire, r1 = multi.protect_host(w.desc, w.plain, w.wire_size)
+    out = np.full(w.wire_size, 0xAA, np.uint8)
+    res = np.zeros(len(w.desc), L.RESULT)
+    multi.protect_into(w.desc, w.plain, out, res)
+    assert np.array_equal(out, wire) and np.array_equal(res, r1)
+    back = np.empty(w.plain_size, np.uint8)
+    res2 = np.zeros(len(w.desc), L.RESULT)
+    multi.unprotect_into(w.udesc, out, back, res2)
+    assert (res2["status"] == 0).all() and np.array_equal(back, w.plain)
