@@ -408,6 +408,31 @@ __device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, const
     return aes_rounds<NR, 1>(u32x4{in.x ^ rk[0], in.y ^ rk[1], in.z ^ rk[2], in.w ^ rk[3]}, rk, T);
 }
 
+// One AES block held by every lane of a quad, computed by the quad jointly
+// (HeaderProtection_mask of a packet, _crypto.c:278-287): lane j keeps state
+// column j and takes the other three columns of each round from its quad
+// neighbours by DPP, so a round costs 4 table lookups per lane instead of 16
+// -- a quarter of the LDS instructions of four private copies.  rk: round
+// keys in memory, column j read by lane j.  Every lane of the quad must be
+// active.  Returns the block in every lane.
+template <int NR, class TE>
+__device__ __forceinline__ u32x4 aes_encrypt_quad(u32x4 in, const uint32_t *rk, const TE &T, int sub)
+{
+    constexpr int kNext1 = 0x39, kNext2 = 0x4E, kNext3 = 0x93;  // lane j <- lane j+1 / j+2 / j+3
+    uint32_t k[NR + 1];
+#pragma unroll
+    for (int r = 0; r <= NR; ++r) k[r] = rk[4 * r + sub];
+    uint32_t s = (sub == 0 ? in.x : sub == 1 ? in.y : sub == 2 ? in.z : in.w) ^ k[0];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        const uint32_t s1 = quad_perm<kNext1>(s), s2 = quad_perm<kNext2>(s), s3 = quad_perm<kNext3>(s);
+        s = xor3(xor3(T.t0(s), T.t1(s1), T.t2(s2)), T.t3(s3), k[r]);
+    }
+    const uint32_t s1 = quad_perm<kNext1>(s), s2 = quad_perm<kNext2>(s), s3 = quad_perm<kNext3>(s);
+    s = (T.f0(s) | T.f1(s1) | T.f2(s2) | T.f3(s3)) ^ k[NR];
+    return u32x4{quad_perm<0x00>(s), quad_perm<0x55>(s), quad_perm<0xAA>(s), quad_perm<0xFF>(s)};
+}
+
 // Counter-mode caching.  Within a packet the GCM counter block is
 // nonce || BE32(cb) with cb < 256 (at most 95 blocks + J0), so only byte 15
 // changes: in round 1 it reaches one output word through one lookup, in

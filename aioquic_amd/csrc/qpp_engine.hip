@@ -127,14 +127,14 @@ __device__ __forceinline__ u32x4 lds_sample(const uint8_t *scr, int s)
 // HeaderProtection_mask (_crypto.c:278-287): AES-ECB(hp, sample), or the
 // first ChaCha20 block with counter = sample[0:4] and nonce = sample[4:16].
 // The same, computed jointly by a packet's quad (every lane holds the same
-// sample): ChaCha20 by columns across the quad; AES as above.
+// sample): ChaCha20 and AES by columns across the quad.
 template <int SUITE, class TE>
 __device__ __forceinline__ u32x4 hp_mask_quad(const KeySlot *ks, u32x4 sample, const TE &T, int sub)
 {
     if constexpr (SUITE == QPP_CHACHA20_POLY1305)
         return chacha_block_quad_row0(ks->hrk, sample.x, sample.y, sample.z, sample.w, sub);
     else
-        return aes_encrypt<SUITE == QPP_AES_256_GCM ? 14 : 10>(sample, ks->hrk, T);
+        return aes_encrypt_quad<SUITE == QPP_AES_256_GCM ? 14 : 10>(sample, ks->hrk, T, sub);
 }
 
 template <int SUITE, class TE>
