@@ -38,6 +38,37 @@ __device__ __forceinline__ void chacha_block(const uint32_t *key, uint32_t ctr, 
     out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
 }
 
+// chacha_block with side(i) called after double round i (i = 0..9), in the
+// same straight-line code: independent work placed there (Poly1305 of the
+// previous chunk) shares a basic block with the rounds, so the scheduler can
+// interleave the two dependency chains.
+template <class SIDE>
+__device__ __forceinline__ void chacha_block_beside(const uint32_t *key, uint32_t ctr, uint32_t n0,
+                                                    uint32_t n1, uint32_t n2, uint32_t out[16], SIDE side)
+{
+    uint32_t x0 = 0x61707865, x1 = 0x3320646e, x2 = 0x79622d32, x3 = 0x6b206574;
+    uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
+    uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
+    uint32_t x12 = ctr, x13 = n0, x14 = n1, x15 = n2;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        QPP_QR(x0, x4, x8, x12);
+        QPP_QR(x1, x5, x9, x13);
+        QPP_QR(x2, x6, x10, x14);
+        QPP_QR(x3, x7, x11, x15);
+        QPP_QR(x0, x5, x10, x15);
+        QPP_QR(x1, x6, x11, x12);
+        QPP_QR(x2, x7, x8, x13);
+        QPP_QR(x3, x4, x9, x14);
+        side(i);
+    }
+    out[0] = x0 + 0x61707865; out[1] = x1 + 0x3320646e;
+    out[2] = x2 + 0x79622d32; out[3] = x3 + 0x6b206574;
+    out[4] = x4 + key[0]; out[5] = x5 + key[1]; out[6] = x6 + key[2]; out[7] = x7 + key[3];
+    out[8] = x8 + key[4]; out[9] = x9 + key[5]; out[10] = x10 + key[6]; out[11] = x11 + key[7];
+    out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
+}
+
 // One ChaCha20 block computed by the 4 lanes of a quad together (all four
 // hold the same inputs): lane j keeps column j (words j, 4+j, 8+j, 12+j), the
 // column rounds are lane-local and the diagonal rounds rotate rows 1-3 by

@@ -62,6 +62,7 @@ template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
     uint8_t stage[WG / 64][kChStage];
     uint8_t scratch[WG / 4][kScratch];
+    uint32_t pw[WG / 4][20];  // per packet: r, r^2, r^3, r^4 (5 limbs each) for the tag's close
 };
 
 // Fill the LDS AES image: row x = [Te0[x] x 32 | Te1[x] x 32], 16-byte stores.
@@ -425,15 +426,17 @@ __device__ __forceinline__ void probe_mark(int i)
 
 // Per-packet state that the GCM step loop does not touch waits in LDS
 // (scratch [64, 96)) while the loop runs, so the loop keeps its 128 VGPRs.
-__device__ __forceinline__ void park(const Pkt &P, uint8_t *scr)
+// mask = false: the HP mask is not parked (a protect computes it after the
+// payload; unpark then returns zeros), so no zero vector is held for it
+__device__ __forceinline__ void park(const Pkt &P, uint8_t *scr, bool mask = true)
 {
-    *(u32x4 *)(scr + kScrPark) = P.mask;
+    if (mask) *(u32x4 *)(scr + kScrPark) = P.mask;
     *(u32x4 *)(scr + kScrPark + 16) =
         u32x4{(uint32_t)P.pn, (uint32_t)(P.pn >> 32),
               P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 | (uint32_t)P.hp << 28,
               (uint32_t)P.hlen | (uint32_t)P.clen << 16};
 }
-__device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, uint8_t *dst)
+__device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, uint8_t *dst, bool mask = true)
 {
     Pkt P;
     const u32x4 w = *(const u32x4 *)(scr + kScrPark + 16);
@@ -441,7 +444,7 @@ __device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, ui
     P.dst = dst;
     P.hlen = (int)(w.w & 0xffff);
     P.clen = (int)(w.w >> 16);
-    P.mask = *(const u32x4 *)(scr + kScrPark);
+    P.mask = mask ? *(const u32x4 *)(scr + kScrPark) : zero4();
     P.pn = (uint64_t)w.y << 32 | w.x;
     P.fbm = w.z & 0xff;
     P.pn_off = (int)((w.z >> 8) & 0xffff);
@@ -794,13 +797,12 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *
 // with the associated data, and one quad sum at the end.  B / ioff / ooff:
 // the wave's buffer views and the packet's offsets in them.
 template <bool ENC>
-__device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, uint8_t *stage,
+__device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, uint8_t *stage, uint32_t *pw,
                               const Bufs &B, uint32_t ioff, uint32_t ooff)
 {
     const uint32_t *key = ks->rk;
     const uint32_t n0 = P.nonce.x, n1 = P.nonce.y, n2 = P.nonce.z;
     const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4;
-    const int n_g = n_a + n_c + 1;
     const int chunks = (P.clen + 63) >> 6;
     const bool unmask = !ENC && P.hp;
     const uint8_t *pin = P.src + P.hlen;
@@ -826,48 +828,48 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
     // the packet fields the chunk loop does not use (HP mask, packet number,
     // header layout) wait in LDS until the tag: 128 VGPRs at 4 waves per SIMD
     // leave no room for them across the loop
-    park(P, scr);
+    park(P, scr, !ENC);
 
     dma(0);
     // r13 = r^13: the multiply of a lane's last block before its next chunk
     // also jumps over the other 3 lanes' chunks (12 blocks), so a chunk costs
     // 4 multiplies instead of 4 + 1
     P130 acc = p130_zero(), r = p130_zero(), r13 = p130_zero();
-    int g_last = -1;
-#pragma unroll 1
-    for (int k = 0; k < steps; ++k) {
-        const int c = 4 * k + sub - 1;  // this lane's chunk (-1: the key block)
-        uint32_t blk[16];
-        chacha_block(key, (uint32_t)(c + 1), n0, n1, n2, blk);
-        if (k == 0) {
-            // one-time key from lane 0: r, and s parked in LDS until the tag
-            uint32_t kw[8];
+    // Poly1305 over the 4 blocks of chunk c (their inputs x), branch-free so
+    // that it shares a basic block with the next ChaCha20 block and the
+    // scheduler can fill the latency of its 64-bit multiply-add chains with
+    // the block's independent quarter rounds.  Blocks that do not exist
+    // (c < 0: the key unit; past the payload's end) multiply by one and add
+    // zero, which leaves the chain as it is.
+    auto poly_blk = [&](const u32x4 (&x)[4], int c, int b) {
+        {
+            const int i = 4 * c + b;
+            const bool valid = c >= 0 && i < n_c;
+            const P130 m = p130_block(x[b]);
+            const P130 &rm = (b == 3 && c + 4 < chunks) ? r13 : r;
+            // (x[b] is zero for a block that does not exist: only the 2^128
+            // bit of p130_block needs masking)
+            P130 a = acc, f;
 #pragma unroll
-            for (int w = 0; w < 8; ++w) kw[w] = quad_dpp<0x00>(blk[w]);
-            *(u32x4 *)(scr + kScrEj0) = u32x4{kw[4], kw[5], kw[6], kw[7]};
-            r = p130_r(kw[0], kw[1], kw[2], kw[3]);
-            const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2);
-            r13 = p130_mul(p130_mul(p130_mul(r4, r4), r4), r);
-            // lane 0 starts its chain with the associated data (its next
-            // chunk, if any, is chunk 3)
-            if (sub == 0) {
-                const Pkt Q = unpark(scr, P.src, P.dst);
-                for (int g = 0; g < n_a; ++g) {
-                    const int nb = min(16, P.hlen - 16 * g);
-                    u32x4 a = (g == 0 && h0) ? keep_bytes(*(const u32x4 *)h0, nb)
-                                             : ld_win(P.src + 16 * g, nb, P.src, P.src + rlen);
-                    if (unmask) a ^= hp_pattern(16 * g, Q.mask, Q.fbm, Q.pn_off, Q.pn_len);
-                    if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
-                    acc = p130_mul(p130_add(acc, p130_block(a)), (g == n_a - 1 && 3 < chunks) ? r13 : r);
-                    g_last = g;
-                }
+            for (int l = 0; l < 5; ++l) {
+                a.v[l] += l < 4 ? m.v[l] : valid ? m.v[l] : 0u;
+                f.v[l] = valid ? rm.v[l] : (l == 0 ? 1u : 0u);
             }
+            acc = p130_mul(a, f);
         }
-        // the lane's chunk from region `sub` (the DMA retires in issue order,
-        // after the previous step's stores: vmcnt(0) waits for both)
+    };
+    auto poly = [&](const u32x4 (&x)[4], int c) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) poly_blk(x, c, b);
+    };
+    // the memory side of step k: the lane's chunk c from region `sub` xor
+    // its keystream, back through LDS to 4 coalesced stores, the next step's
+    // LDS-DMA; x = the chunk's Poly1305 inputs
+    auto chunk_io = [&](int k, int c, const uint32_t (&blk)[16], u32x4 (&x)[4]) {
+        // (the DMA retires in issue order, after the previous step's stores:
+        // vmcnt(0) waits for both)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint8_t *mine = stage + sub * kChRegion + qoff;
-        u32x4 x[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const int i = 4 * c + b;
@@ -910,45 +912,102 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         if (k + 1 < steps) dma(k + 1);
-        if (c >= 0 && c < chunks) {
+    };
+
+    // step 0: unit `sub` (lane 0: the one-time key, lanes 1-3: chunks 0-2)
+    u32x4 x[4];
+    {
+        uint32_t blk[16];
+        chacha_block(key, (uint32_t)sub, n0, n1, n2, blk);
+        // one-time key from lane 0: r, and s parked in LDS until the tag
+        uint32_t kw[8];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                if (4 * c + b >= n_c) break;
-                // block 3 of a chunk the lane follows with chunk c + 4: r^13
-                acc = p130_mul(p130_add(acc, p130_block(x[b])), (b == 3 && c + 4 < chunks) ? r13 : r);
-                g_last = n_a + 4 * c + b;
+        for (int w = 0; w < 8; ++w) kw[w] = quad_dpp<0x00>(blk[w]);
+        *(u32x4 *)(scr + kScrEj0) = u32x4{kw[4], kw[5], kw[6], kw[7]};
+        r = p130_r(kw[0], kw[1], kw[2], kw[3]);
+        const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2);
+        r13 = p130_mul(p130_mul(p130_mul(r4, r4), r4), r);
+        if (sub == 0) {
+            const P130 r3 = p130_mul(r2, r);
+#pragma unroll
+            for (int l = 0; l < 5; ++l) {
+                pw[l] = r.v[l];
+                pw[5 + l] = r2.v[l];
+                pw[10 + l] = r3.v[l];
+                pw[15 + l] = r4.v[l];
             }
         }
+        // lane 0 starts its chain with the associated data (its next chunk,
+        // if any, is chunk 3)
+        if (sub == 0) {
+            const Pkt Q = unpark(scr, P.src, P.dst, !ENC);
+            for (int g = 0; g < n_a; ++g) {
+                const int nb = min(16, P.hlen - 16 * g);
+                u32x4 a = (g == 0 && h0) ? keep_bytes(*(const u32x4 *)h0, nb)
+                                         : ld_win(P.src + 16 * g, nb, P.src, P.src + rlen);
+                if (unmask) a ^= hp_pattern(16 * g, Q.mask, Q.fbm, Q.pn_off, Q.pn_len);
+                if (!ENC || !P.hp) st_part(P.dst + 16 * g, a, nb);
+                acc = p130_mul(p130_add(acc, p130_block(a)), (g == n_a - 1 && 3 < chunks) ? r13 : r);
+            }
+        }
+        chunk_io(0, sub - 1, blk, x);
     }
+    // step k: the ChaCha20 block of unit 4k + sub beside Poly1305 of the
+    // lane's previous chunk (software-pipelined by one step)
+#pragma unroll 1
+    for (int k = 1; k < steps; ++k) {
+        const int c = 4 * k + sub - 1;
+        uint32_t blk[16];
+        // the previous chunk's 4 Poly1305 blocks after double rounds 1, 3, 5, 7
+        chacha_block_beside(key, (uint32_t)(c + 1), n0, n1, n2, blk, [&](int i) {
+            if (i & 1 && i < 8) poly_blk(x, c - 4, i >> 1);
+        });
+        // pin the chain here: otherwise the compiler sinks this Poly1305 step
+        // to the next iteration's top (beside the loop's exit test), out of
+        // the rounds' basic block
+        acc = launder(acc);
+        chunk_io(k, c, blk, x);
+    }
+    poly(x, 4 * (steps - 1) + sub - 1);
     {
         const uint8_t *src = P.src;
         uint8_t *dst = P.dst;
-        P = unpark(scr, src, dst);
+        P = unpark(scr, src, dst, !ENC);
     }
-    // acc = sum m_g r^(g_last - g + 1); scale to r^(n_g - g) with r^(n_g - 1 - g_last)
-    int e = n_g - 1 - g_last;
-    if (g_last < 0) e = 0;
-    P130 f = acc;
-    if (e > 1) {
-        const P130 rr = launder(r);
-        const P130 r2 = p130_mul(rr, rr), r4 = p130_mul(r2, r2), r8 = p130_mul(r4, r4);
-        const int m = e - 1;
-        if (m & 1) f = p130_mul(f, rr);
-        if (m & 2) f = p130_mul(f, r2);
-        if (m & 4) f = p130_mul(f, r4);
-        if (m & 8) f = p130_mul(f, r8);
-        if (m & 16) f = p130_mul(f, p130_mul(r8, r8));
+    // Close the four chains in one Horner pass over the quad.  Lane j's chain
+    // ends at the last block of its last chunk (lane 0 without a chunk: the
+    // last header block, position -1); the lanes' ends follow one another in
+    // the order L + 1, L + 2, L + 3, L (mod 4), L = chunks mod 4 holding the
+    // final chunk, 4 blocks apart except the final chunk's nb blocks:
+    //   S = ((A[L+1] r^4 + A[L+2]) r^4 + A[L+3]) r^nb + A[L]
+    // (a lane with no block at all holds 0).  Every lane computes S from the
+    // quad's chains exchanged through the (now idle) staging regions and the
+    // packet's r^2..r^4 parked in LDS at the key block.
+    {
+        uint8_t *q0 = stage + qoff, *q1 = stage + kChRegion + qoff;
+        *(u32x4 *)(q0 + 16 * sub) = u32x4{acc.v[0], acc.v[1], acc.v[2], acc.v[3]};
+        *(uint32_t *)(q1 + 4 * sub) = acc.v[4];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
     }
-    P130 sum;
+    auto chain = [&](int j) -> P130 {
+        const u32x4 v = *(const u32x4 *)(stage + qoff + 16 * (j & 3));
+        return P130{{v.x, v.y, v.z, v.w, *(const uint32_t *)(stage + kChRegion + qoff + 4 * (j & 3))}};
+    };
+    auto power = [&](int e) -> P130 {  // r^e, e = 1..4
+        P130 x;
 #pragma unroll
-    for (int l = 0; l < 5; ++l) {
-        uint32_t v = f.v[l];
-        v += quad_perm<kQuadSwap1>(v);
-        v += quad_perm<kQuadSwap2>(v);
-        sum.v[l] = v;
-    }
+        for (int l = 0; l < 5; ++l) x.v[l] = pw[5 * (e - 1) + l];
+        return x;
+    };
+    const int L = chunks & 3;
+    const int nb = chunks > 0 ? n_c - 4 * (chunks - 1) : 1;
+    const P130 r4 = power(4);
+    P130 sum = p130_add(p130_mul(chain(L + 1), r4), chain(L + 2));
+    sum = p130_add(p130_mul(sum, r4), chain(L + 3));
+    sum = p130_add(p130_mul(sum, power(nb)), chain(L));
     const u32x4 lens = u32x4{(uint32_t)P.hlen, 0u, (uint32_t)P.clen, 0u};
-    sum = p130_mul(p130_add(sum, p130_block(lens)), r);
+    sum = p130_mul(p130_add(sum, p130_block(lens)), power(1));
     const u32x4 sw = *(const u32x4 *)(scr + kScrEj0);
     const u32x4 tag = p130_finish(sum, sw.x, sw.y, sw.z, sw.w);
     if (ENC) {
@@ -1376,7 +1435,7 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
                 const Bufs B{
                     __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
                     __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
-                chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2], sm.stage[tf >> 6], B, (uint32_t)ioff,
+                chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2], sm.stage[tf >> 6], sm.pw[tf >> 2], B, (uint32_t)ioff,
                                    (uint32_t)ooff);
             }
             write_result<ENC>(res, planned ? desc[p1].rsv : p1, lane_fresh() & 3, P);
