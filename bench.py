@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
     ap.add_argument("--order", choices=("grouped", "round_robin", "random"), default=None,
                     help="override the config's arrival order (non-grouped orders are bucketed)")
+    ap.add_argument("--keys", type=int, default=0, help="study knob: override the config's key count")
     ap.add_argument("--layout", choices=("arrival", "by_key"), default="arrival",
                     help="study knob: by_key stores each key's packets contiguously")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -385,6 +386,9 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")
     cfg = dict(CONFIGS[args.config])
+    if args.keys:
+        cfg["n_keys"] = args.keys
+        cfg["name"] = cfg["name"].replace(f"{CONFIGS[args.config]['n_keys']} key", f"{args.keys} key")
     if args.order:
         cfg["order"] = args.order
         cfg["name"] += f" [{args.order} order]"
