@@ -146,8 +146,7 @@ int main(int argc, char **argv)
                (double)n * 1200 / ((tp + tu) * 1e-3) / (1u << 30));
         return 0;
     }
-    const int wg = suite == QPP_CHACHA20_POLY1305 ? wg_choice("QPP_WG_CHACHA_ENC", kChachaWGEnc, true)
-                                                  : wg_choice("QPP_WG_GCM", kGcmWG, false);
+    const int wg = suite == QPP_CHACHA20_POLY1305 ? kChachaWG : kGcmWG;
 #ifdef QPP_PROBE
     std::vector<unsigned long long> pr((size_t)kProbeWaves * kProbeSlots);
 #endif
