@@ -39,7 +39,7 @@ constexpr int kSetupWG = 256;
 // E_K(J0); [64, 96) the parked packet view (GCM step loop); [96, 112) input
 // bytes [0, 16) (the first header block) for the header write.
 constexpr int kScratch = 112;
-constexpr int kScrTail = 32, kScrEj0 = 48, kScrPark = 64, kScrHdr = 96;
+constexpr int kScrEj0 = 48, kScrPark = 64, kScrHdr = 96;
 constexpr uint32_t kNoSlot = 0xffffffffu;
 // Descriptor flag set by the host session for a descriptor whose extents do
 // not fit the caller's buffers: the packet reports QPP_S_LENGTH and no byte
@@ -424,8 +424,8 @@ __device__ __forceinline__ void probe_mark(int i)
 #define QPP_PROBE_AT(i) ((void)0)
 #endif
 
-// Per-packet state that the GCM step loop does not touch waits in LDS
-// (scratch [64, 96)) while the loop runs, so the loop keeps its 128 VGPRs.
+// Per-packet state that the ChaCha20-Poly1305 slot loop does not touch waits
+// in LDS (scratch [64, 96)) while the loop runs, so the loop keeps its VGPRs.
 // mask = false: the HP mask is not parked (a protect computes it after the
 // payload; unpark then returns zeros), so no zero vector is held for it
 __device__ __forceinline__ void park(const Pkt &P, uint8_t *scr, bool mask = true)
@@ -455,30 +455,10 @@ __device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, ui
     return P;
 }
 
-// AES-GCM of one packet by its quad (SP 800-38D; _crypto.c:157-204 / :115-155).
-//   * The associated data (header) is first folded to one block
-//     Z = sum_g A_g H^(n_a-1-g) by every lane of the quad; GHASH is linear, so
-//     Z then stands for the whole header as the first block of the sequence
-//     [Z | CT | lengths] that the step loop walks (front-padded to 4S).
-//   * Step k: lane `sub` owns block 4k+sub: one AES-CTR block (rounds 1-2 from
-//     the packet's counter cache), one LDS-DMA load of next step's input
-//     block (the received tag on the last step) into the wave's staging
-//     buffer, one buffer store (dropped out of range for partial blocks), one
-//     H^4 multiply.
-//   * Partial tail block -> LDS, E_K(J0) -> LDS; both go out after the loop.
-// The input region holds >= 16 bytes except for tiny protects, which are
-// staged in LDS.  Returns the tag; got_tag = the received tag (unprotect).
-// Inside the step loop every lane-derived address (LDS table lane offset,
-// staging slot, packet scratch) is recomputed from lane_fresh(): 128 VGPRs
-// leave no room to keep them live.  scr_wave = the wave's 16 packet
-// scratches, stage = the wave's 2 staging buffers, te = the AES image.
-// GHASH tables of the packet's key slot.  The step loop multiplies by H^4
-// from one of the workgroup's LDS table entries (8 KiB each at LDS offset 0;
-// ghash_mul_lds selects the entry in its v_perm).  The few multiplies outside
-// the loop (associated data beyond 16 bytes by H^1, each lane's closing
-// H^(4-j)) read the slot's tables in global memory, so that LDS holds H^4
-// alone and four connections' tables fit beside the AES image.  The wave's
-// slot and entry live in LDS, re-read where needed rather than kept in SGPRs.
+// GHASH tables of a GCM packet's key slot: the step loop's H^4 from one of
+// the workgroup's LDS table entries, the few other powers from the slot's
+// tables in global memory (gcm_packet).  The wave's slot and entry live in
+// LDS, re-read where needed rather than kept in SGPRs.
 struct GhashTabs {
     const uint8_t *lds;     // LDS table entries
     const uint8_t *gtab;    // every slot's tables, global memory
@@ -507,16 +487,87 @@ __device__ __forceinline__ int gcm_pad(int n_g)
     return QS * ((n_g + QS - 1) / QS) - n_g;
 }
 
-template <int NR, bool ENC, int BPL>
-__device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int clen,
-                                            const uint32_t *rk, int sub, uint8_t *scr,
-                                            uint8_t *scr_wave, const GhashTabs &G,
-                                            const uint8_t *te, const Bufs &B,
-                                            const uint8_t *src, uint32_t ioff, uint32_t ooff,
-                                            const u32x4 hmask, const uint32_t hbits, const u32x4 h0,
+// Protect with header protection: the HP sample lies in CT blocks 0 and 1
+// (sample = ct[4-pn_len, 20-pn_len), _crypto.c:302).  When both blocks are
+// written by the quad's first step (BPL = 2: positions q = pad + za and
+// q + 1 within the first 8) and the sample lies inside the ciphertext, the
+// quad takes them by DPP in that step, computes the mask and writes the
+// header there ("fast"); otherwise the sample is read back from the output
+// after the step loop.
+template <int BPL>
+__device__ __forceinline__ bool gcm_fast_hp(int hlen, int clen)
+{
+    if constexpr (BPL != 2) {
+        return false;
+    } else {
+        const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
+        return gcm_pad<BPL>(za + n_c + 1) + za <= 6 && clen >= 19;
+    }
+}
+
+// n (0..15) bytes of v to buffer offset off (a partial tail block, stored by
+// the lane that computed it inside the step loop).
+__device__ __forceinline__ void buf_st_part(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v, int n)
+{
+    const int nd = n >> 2, rb = n & 3;
+    if (nd > 0) __builtin_amdgcn_raw_buffer_store_b32(v.x, r, (int)off, 0, 0);
+    if (nd > 1) __builtin_amdgcn_raw_buffer_store_b32(v.y, r, (int)off + 4, 0, 0);
+    if (nd > 2) __builtin_amdgcn_raw_buffer_store_b32(v.z, r, (int)off + 8, 0, 0);
+    if (rb) {
+        uint32_t t = nd == 0 ? v.x : nd == 1 ? v.y : nd == 2 ? v.z : v.w;
+        const int o = (int)off + 4 * nd;
+        if (rb & 2) {
+            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)t, r, o, 0, 0);
+            t >>= 16;
+        }
+        if (rb & 1) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)t, r, o + (rb & 2), 0, 0);
+    }
+}
+
+// The header out, block q of it by lane q (mod 4): the input header with the
+// HP mask applied (protect) or removed (unprotect), or as is (no HP).  h0 =
+// the input's first 16 bytes (have_h0), other blocks are read from P.src.
+__device__ __forceinline__ void write_header_v(const Pkt &P, int sub, bool masked, int rlen, u32x4 h0,
+                                               bool have_h0)
+{
+    const int n_a = (P.hlen + 15) >> 4;
+    for (int q = sub; q < n_a; q += 4) {
+        const int nb = min(16, P.hlen - 16 * q);
+        u32x4 h = (q == 0 && have_h0) ? h0 : ld_win(P.src + 16 * q, nb, P.src, P.src + rlen);
+        if (masked) h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
+        st_part(P.dst + 16 * q, h, nb);
+    }
+}
+
+// AES-GCM of one packet by its quad (SP 800-38D; _crypto.c:157-204 / :115-155).
+//   * The associated data (header) is first folded to one block
+//     Z = sum_g A_g H^(n_a-1-g) by every lane of the quad; GHASH is linear, so
+//     Z then stands for the whole header as the first block of the sequence
+//     [Z | CT | lengths] that the step loop walks (front-padded to 8S).
+//   * Step k: lane `sub` owns blocks 8k+sub and 8k+4+sub: their AES-CTR
+//     keystream (rounds 1-2 from the packet's counter cache), the register
+//     prefetch of the next step's input, two buffer stores (dropped out of
+//     range; a partial tail block is stored by its lane with byte stores), two
+//     H^4 multiplies.
+//   * Nothing of a packet waits in LDS: unprotect writes its header before the
+//     loop (the mask is known), protect in its first step (gcm_fast_hp) or
+//     after the loop; E_K(J0) stays in the lengths lane's registers.
+// The input region holds >= 16 bytes except for tiny packets (< 16 bytes),
+// whose input is loaded once by a partial load.  Returns the tag; got_tag =
+// the received tag (unprotect).  Inside the step loop every lane-derived value
+// is recomputed from lane_fresh(): at 128 VGPRs nothing else stays live.
+// GHASH tables of the packet's key slot: the step loop multiplies by H^4 from
+// one of the workgroup's LDS table entries; the few multiplies outside the
+// loop (associated data beyond 16 bytes by H^1, each lane's closing H^(4-j))
+// read the slot's tables in global memory.
+template <int NR, bool ENC, int BPL, int SUITE>
+__device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, const u32x4 h0,
+                                            const uint32_t *rk, int sub, const GhashTabs &G,
+                                            const uint8_t *te, const Bufs &B, uint32_t ioff, uint32_t ooff,
                                             u32x4 &got_tag)
 {
     const LdsTe T{te, (lane_fresh() & 31) * 4};
+    const int hlen = P.hlen, clen = P.clen;
     const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
     const int n_g = za + n_c + 1, pad = gcm_pad<BPL>(n_g), S = (n_g + pad) / (4 * BPL);
     const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
@@ -524,15 +575,14 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
     // the H^4 entry, read once: an LDS read inside the step loop would make
     // every step wait for all of its outstanding table lookups
     const uint32_t t4 = G.t4();
-
-    if (tiny) *(u32x4 *)(scr + kScrTail) = ld_part(src, rlen);
+    const u32x4 tiny_in = tiny ? ld_part(P.src, rlen) : zero4();
 
     // fold the associated data (unmasked for unprotect) into Z
     u32x4 z = {0, 0, 0, 0};
     for (int g = 0; g < n_a; ++g) {
         u32x4 a;
         if (tiny) {
-            a = *(const u32x4 *)(scr + kScrTail);
+            a = tiny_in;
         } else if (g == 0) {
             a = h0;  // requested with the descriptor
         } else {
@@ -542,68 +592,36 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                           16 * g - ld);
         }
         a = keep_bytes(a, min(16, hlen - 16 * g));
-        if (!ENC && (hbits >> 28))
-            a ^= hp_pattern(16 * g, hmask, hbits & 0xff, (hbits >> 8) & 0xffff, (hbits >> 24) & 0xf);
+        if (!ENC && P.hp) a ^= hp_pattern(16 * g, P.mask, P.fbm, P.pn_off, P.pn_len);
         if (g > 0) z = ghash_mul_global(z, G.global(0));  // H^1
         z ^= a;
     }
+    // the header out: unprotect (mask known) and protect without HP now;
+    // protect with HP in its first step or after the loop
+    if (!ENC || !P.hp) write_header_v(P, sub, !ENC && P.hp, rlen, tiny ? tiny_in : h0, true);
+    const bool fast_hp = ENC && P.hp && gcm_fast_hp<BPL>(hlen, clen);
     // BPL = 1: Z enters as lane `pad`'s initial accumulator (position pad is
     // in its first step's only block); BPL = 2: Z may sit at the second block
     // of a lane's first step, so it enters through that step's input (step2)
     u32x4 acc = (BPL == 1 && za && sub == pad) ? z : u32x4{0, 0, 0, 0};
     const int q = pad + za;  // sequence position of CT block 0
-    // E_K(J0) slot starts at zero: lanes other than the lengths lane add 0
-    *(u32x4 *)(scr + kScrEj0) = zero4();
-    const CtrCache cc = ctr_cache(nonce, rk, T);
+    const CtrCache cc = ctr_cache(P.nonce, rk, T);
     const uint32_t lens_h = bswap((uint32_t)hlen * 8u);
     const uint32_t cin = ioff + (uint32_t)hlen, cout = ooff + (uint32_t)hlen;
 
-    // one block of the sequence: CT block i (input `raw` loaded from CT offset
-    // min(16 i, clen - 16) for protect, i.e. end-aligned for a partial tail),
-    // the lengths block (i == n_c), or padding
-    auto step = [&](int i, bool last, auto first_c, u32x4 raw) {
-        constexpr bool first = decltype(first_c)::value;
-        const bool is_ct = i >= 0 && 16 * i < clen;
-        const LdsTe Tl{te, (lane_fresh() & 31) * 4};
-        const uint32_t cb = is_ct ? (uint32_t)(i + 2) : 1u;
-        (void)first;
-        const u32x4 ksb = aes_ctr<NR>(cc, cb, rk, Tl);
-        u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
-        uint32_t soff = kOob;
-        if (is_ct) {
-            const int nb = clen - 16 * i;
-            if (__builtin_expect(nb >= 16, 1)) {
-                // a full block: no byte shifts or masks (a branch, skipped by
-                // the waves whose lanes hold no partial block this step)
-                out = raw ^ ksb;
-                x = ENC ? out : raw;
-                soff = cout + 16u * (uint32_t)i;
-            } else {
-                const u32x4 cur = ENC ? shr_bytes(raw, 16 - nb) : raw;
-                out = cur ^ ksb;
-                x = keep_bytes(ENC ? out : cur, nb);
-                *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrTail) = out;
-            }
-            if (ENC && i < 2) *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + 16 * i) = x;
-        } else if (i >= 0 && 16 * i < clen + 16) {
-            // lengths block; this lane's AES slot produced E_K(J0) for the tag
-            x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
-            *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, 0);
-        acc ^= x;
-        __builtin_amdgcn_sched_barrier(0);
-        // H^4 inside the loop (resident LDS table); the last step's H^(4-j)
-        // is applied after the loop
-        if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
+    // The last step: lane j closes its Horner chain with H^(4-j) (the slot's
+    // global table of power 3 - j), and the lengths block's lane (lane 3, the
+    // last position of the sequence) adds E_K(J0), which its AES slot just
+    // produced (keystream ksl): the tag is then the quad's xor of acc
+    auto close = [&](u32x4 ksl) {
+        const uint32_t lf = lane_fresh();
+        acc = ghash_mul_global(acc, G.global(3u - (lf & 3)));
+        if ((lf & 3) == 3) acc ^= ksl;
     };
-    // buffer offset of CT block i's input (or out of range)
-    auto ct_load = [&](int i) -> uint32_t {
-        if (i < 0 || 16 * i >= clen) return kOob;
-        return cin + (uint32_t)(ENC ? min(16 * i, clen - 16) : 16 * i);
-    };
-    // BPL = 2: the output side of one block (as in `step`) given its keystream;
-    // returns the GHASH input of the block
+    // the output side of one block given its keystream: CT block i (input
+    // `raw` loaded from CT offset min(16 i, clen - 16) for protect, i.e.
+    // end-aligned for a partial tail), the lengths block (i == n_c), or
+    // padding; returns the GHASH input of the block
     auto blk_out = [&](int i, u32x4 ksb, u32x4 raw) -> u32x4 {
         const bool is_ct = i >= 0 && 16 * i < clen;
         u32x4 x = {0, 0, 0, 0}, out = {0, 0, 0, 0};
@@ -620,15 +638,26 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                 const u32x4 cur = ENC ? shr_bytes(raw, 16 - nb) : raw;
                 out = cur ^ ksb;
                 x = keep_bytes(ENC ? out : cur, nb);
-                *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrTail) = out;
+                buf_st_part(B.out, cout + 16u * (uint32_t)i, out, nb);
             }
-            if (ENC && i < 2) *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + 16 * i) = x;
         } else if (i >= 0 && 16 * i < clen + 16) {
+            // lengths block; this lane's AES slot produced E_K(J0) (close)
             x = u32x4{0u, lens_h, 0u, bswap((uint32_t)clen * 8u)};
-            *(u32x4 *)(scr_wave + (lane_fresh() >> 2) * kScratch + kScrEj0) = ksb;
         }
         __builtin_amdgcn_raw_buffer_store_b128(out, B.out, (int)soff, 0, 0);
         return x;
+    };
+    // one block (BPL = 1)
+    auto step = [&](int i, bool last, auto first_c, u32x4 raw) {
+        (void)first_c;
+        const LdsTe Tl{te, (lane_fresh() & 31) * 4};
+        const bool is_ct = i >= 0 && 16 * i < clen;
+        const u32x4 ksb = aes_ctr<NR>(cc, is_ct ? (uint32_t)(i + 2) : 1u, rk, Tl);
+        acc ^= blk_out(i, ksb, raw);
+        __builtin_amdgcn_sched_barrier(0);
+        // H^4 inside the loop (resident LDS table); the last step closes
+        if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
+        else close(ksb);
     };
     // BPL = 2: lane blocks i and i + 4 (CT indices) in one step
     auto step2 = [&](int i, bool last, u32x4 raw0, u32x4 raw1, auto first_c) {
@@ -648,6 +677,23 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         u32x4 x0 = blk_out(i, ks0, raw0);
         u32x4 x1 = blk_out(i + 4, ks1, raw1);
         if constexpr (first) {
+            if constexpr (ENC) {
+                if (fast_hp) {
+                    // CT blocks 0 and 1 from the lanes that hold them
+                    u32x4 c0 = (i == 0) ? x0 : (i + 4 == 0) ? x1 : zero4();
+                    u32x4 c1 = (i == 1) ? x0 : (i + 4 == 1) ? x1 : zero4();
+                    c0 = quad_xor_all(c0);
+                    c1 = quad_xor_all(c1);
+                    const int s = 4 - P.pn_len;
+                    const u32x4 smp = {__builtin_amdgcn_alignbyte(c0.y, c0.x, s),
+                                       __builtin_amdgcn_alignbyte(c0.z, c0.y, s),
+                                       __builtin_amdgcn_alignbyte(c0.w, c0.z, s),
+                                       __builtin_amdgcn_alignbyte(c1.x, c0.w, s)};
+                    Pkt H = P;
+                    H.mask = hp_mask_quad<SUITE>(ks, smp, Tl, sub);
+                    write_header_v(H, sub, true, rlen, h0, true);
+                }
+            }
             // position q - 1 = pad holds Z (zero without associated data)
             if (i == -1) x0 ^= z;
             if (i + 4 == -1) x1 ^= z;
@@ -657,13 +703,19 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         if (first && pad >= 4) acc = x1;
         else acc = ghash_mul_h4(acc ^ x0, G.lds, t4) ^ x1;
         if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
+        else close(ks1);
+    };
+    // buffer offset of CT block i's input (or out of range)
+    auto ct_load = [&](int i) -> uint32_t {
+        if (i < 0 || 16 * i >= clen) return kOob;
+        return cin + (uint32_t)(ENC ? min(16 * i, clen - 16) : 16 * i);
     };
 
     got_tag = u32x4{0, 0, 0, 0};
     if constexpr (BPL == 2) {
         if (tiny) {
             QPP_PROBE_AT(4);
-            const u32x4 st = shl_bytes(*(const u32x4 *)(scr + kScrTail), 16 - rlen);
+            const u32x4 st = shl_bytes(tiny_in, 16 - rlen);
             step2(sub - q, true, st, st, std::true_type{});
         } else {
             int i = sub - q;
@@ -680,25 +732,22 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
                 i += 8;
             };
             QPP_PROBE_AT(4);
-            // the first step is peeled: it alone may carry Z
+            // the first step is peeled: it alone may carry Z and the HP sample
             one2(S, std::true_type{});
 #pragma unroll 1
             for (int k = S - 1; k > 0; --k) one2(k, std::false_type{});
             if (!ENC) got_tag = nxt0;
         }
     } else if (tiny) {
-        // < 16 input bytes: one step (n_a, n_c <= 1), input from LDS
+        // < 16 input bytes: one step (n_a, n_c <= 1)
         QPP_PROBE_AT(4);
-        // the staged bytes as an end-aligned load would see them
-        const u32x4 st = *(const u32x4 *)(scr + kScrTail);
-        step(sub - q, true, std::true_type{}, shl_bytes(st, 16 - rlen));
+        step(sub - q, true, std::true_type{}, shl_bytes(tiny_in, 16 - rlen));
     } else {
         int i = sub - q;
         // one step: this step's input block, the next step's load (on the
         // last step the received tag), the block.  Register prefetch, one
-        // step ahead (4 VGPRs; the compiler counts vmcnt, so the previous
-        // step's store stays in flight).  The input of the step after step k (counting down to 1; step 0 is
-        // the received tag of an unprotect), block j = i + 4 (S - k)
+        // step ahead.  The input of the step after step k (counting down to
+        // 1; step 0 is the received tag of an unprotect), block j = i + 4 (S - k)
         auto in_of = [&](int k, int j) -> uint32_t {
             return (!ENC && k == 0) ? cin + (uint32_t)clen : ct_load(j);
         };
@@ -716,41 +765,46 @@ __device__ __forceinline__ u32x4 gcm_packet(const u32x4 nonce, int hlen, int cle
         if (!ENC) got_tag = nxt;
     }
     QPP_PROBE_AT(5);
-    // lane-derived values recomputed after the loop rather than kept (spilled)
-    const uint32_t lf = lane_fresh();
-    // lane j closes its Horner chain with H^(4-j) (the slot's global table
-    // of power 3 - j): sum_j acc_j H^(4-j) after the quad's xor
-    acc = ghash_mul_global(acc, G.global(3u - (lf & 3)));
-    // the lengths block is the last of the sequence: lane 3, last step
-    __builtin_amdgcn_wave_barrier();
-    if ((lf & 3) == 3) acc ^= *(const u32x4 *)(scr_wave + (lf >> 2) * kScratch + kScrEj0);
     return quad_xor_all(acc);
 }
 
-// Output side of a GCM packet after the step loop: partial tail block, tag,
-// header (with header protection for protect), tag check for unprotect.
+// Output side of a GCM packet after the step loop: the tag (protect), the
+// header when the first step could not write it (gcm_fast_hp), the tag check
+// for unprotect.  P: re-derived from the descriptor (src, dst, hlen, clen, hp).
 template <bool ENC, int SUITE, int BPL>
-__device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr,
-                                           const LdsTe &T, u32x4 tag, u32x4 got_tag)
+__device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, const LdsTe &T, u32x4 tag,
+                                           u32x4 got_tag)
 {
-    const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
-    const int n_g = za + n_c + 1, pad = gcm_pad<BPL>(n_g);
-    if ((P.clen & 15) && sub == ((pad + za + n_c - 1) & 3))
-        st_part(P.dst + P.hlen + 16 * (n_c - 1), *(const u32x4 *)(scr + kScrTail), P.clen & 15);
-    // input bytes [0, 16) parked in LDS by the prologue (absent for tiny input)
-    const uint8_t *h0 = (P.hlen + P.clen + (ENC ? 0 : QPP_TAG_LEN) >= 16) ? scr + kScrHdr : nullptr;
     if (ENC) {
         if (sub == 0) st16(P.dst + P.hlen + P.clen, tag);
-        if (P.hp) protect_finish_hp<SUITE>(P, ks, sub, scr, tag, T, h0);
-        else write_header(P, sub, false, P.hlen + P.clen, h0);
+        if (P.hp && !gcm_fast_hp<BPL>(P.hlen, P.clen)) {
+            // the header's first byte decides pn_len (HeaderProtection.apply,
+            // _crypto.c:298-302); the sample is read back from the output once
+            // this wave's ciphertext and tag stores have completed (a
+            // coherent load: another lane of the quad may have stored it)
+            const int rlen = P.hlen + P.clen;
+            const bool have = rlen >= 16;
+            const u32x4 hb = have ? ld16(P.src) : ld_part(P.src, rlen);
+            const uint32_t b0 = hb.x & 0xff;
+            P.pn_len = (int)(b0 & 3) + 1;
+            P.pn_off = P.hlen - P.pn_len;
+            P.fbm = first_byte_mask(b0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const __amdgpu_buffer_rsrc_t r =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(P.dst + P.hlen), 0, 64, 0x00020000);
+            const u32x4 smp = __builtin_amdgcn_raw_buffer_load_b128(r, 4 - P.pn_len, 0, 1);
+            P.mask = hp_mask_quad<SUITE>(ks, smp, T, sub);
+            write_header_v(P, sub, true, rlen, hb, true);
+        }
     } else {
+        const int n_a = (P.hlen + 15) >> 4, n_c = (P.clen + 15) >> 4, za = n_a > 0 ? 1 : 0;
+        const int pad = gcm_pad<BPL>(za + n_c + 1);
         const u32x4 diff = got_tag ^ tag;
         if ((diff.x | diff.y | diff.z | diff.w) != 0) {
             P.status = QPP_S_DECRYPT;
             // CT block i sits at sequence position pad + za + i (gcm_packet)
             wipe_payload(P, sub, [&](int i) { return (pad + za + i) & 3; });
         }
-        write_header(P, sub, P.hp, P.hlen + P.clen + QPP_TAG_LEN, h0);
     }
 }
 
@@ -1064,18 +1118,18 @@ __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int su
 constexpr int kTabEntries = 4;
 static_assert(kGhLdsEntry % 1024 == 0, "LDS-DMA pieces of 1 KiB");
 
-template <int WG>
+template <int WG, int NE = kTabEntries>
 struct __attribute__((aligned(16))) GcmSmem {
-    // GHASH table entries first (LDS offset 0: ghash_mul_lds adds e * 8 KiB in
-    // its v_perm), then the AES image at 32 KiB; both within the 16-bit
-    // ds_read immediate range
-    uint8_t h4[kTabEntries][kGhLdsEntry];     // 56 KiB
+    // GHASH table entries first (LDS offset 0: the entry's offset rides in
+    // the 5-bit window address), then the AES image, whose base stays within
+    // the 16-bit ds_read immediate range
+    uint8_t h4[NE][kGhLdsEntry];              // 14 KiB each
     uint8_t te[kTeBytes];                     // Te0|Te1 x 32 bank copies   64 KiB
-    uint8_t scratch[WG / 4][kScratch];
-    uint32_t eslot[kTabEntries];              // slot held by entry e (kNoSlot: none)
-    uint32_t eref[kTabEntries];               // waves running entry e's slot
-    uint32_t eready[kTabEntries];             // entry e's table has landed
-    uint32_t eused[kTabEntries];              // last acquisition (LRU tick)
+    uint32_t eslot[NE];                       // slot held by entry e (kNoSlot: none)
+    uint32_t eref[NE];                        // waves running entry e's slot
+    uint32_t eready[NE];                      // entry e's table has landed
+    uint32_t eused[NE];                       // last acquisition (LRU tick)
+
     uint32_t lock, tick, next;                // entry lock; LRU clock; next item of the share
     uint32_t wslot[WG / 64];                  // per wave: the slot it is running
     uint32_t went[WG / 64];                   // per wave: that slot's table entry
@@ -1267,29 +1321,35 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
                     const Bufs B{
                         __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
                         __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
-                    uint8_t *scr = sm.scratch[t1 >> 2];
-                    const int hlen = P.hlen, clen = P.clen;
-                    const uint32_t hbits = P.fbm | (uint32_t)P.pn_off << 8 | (uint32_t)P.pn_len << 24 |
-                                           (uint32_t)P.hp << 28;
-                    park(P, scr);
-                    *(u32x4 *)(scr + kScrHdr) = pre.h0;
-                    QPP_PROBE_AT(3);
                     const GhashTabs G{&sm.h4[0][0], gtab, &sm.wslot[wv], &sm.went[wv]};
+                    QPP_PROBE_AT(3);
+                    // unprotect: what the results need after the loop
+                    const uint64_t pn = P.pn;
+                    const int hlen = P.hlen;
                     u32x4 got_tag;
-                    const u32x4 tag = gcm_packet<kNR, ENC, BPL>(
-                        P.nonce, hlen, clen, rk, t1 & 3, scr, sm.scratch[wv * 16], G, sm.te, B, P.src,
-                        (uint32_t)ioff, (uint32_t)ooff, P.mask, hbits, pre.h0,
-                        got_tag);
+                    const u32x4 tag = gcm_packet<kNR, ENC, BPL, SUITE>(P, ks, pre.h0, rk, t1 & 3, G, sm.te, B,
+                                                                       (uint32_t)ioff, (uint32_t)ooff, got_tag);
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
                     const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
                     const qpp_desc d2 = desc[p2];
-                    uint8_t *scr2 = sm.scratch[t2 >> 2];
-                    P = unpark(scr2, gin + d2.in_off, gout + d2.out_off);
+                    Pkt Q;
+                    Q.src = gin + d2.in_off;
+                    Q.dst = gout + d2.out_off;
+                    Q.hp = !(d2.flags & QPP_F_NO_HP);
+                    Q.status = QPP_S_OK;
+                    Q.hlen = ENC ? (int)d2.hdr_len : hlen;
+                    Q.clen = ENC ? (int)d2.len : (int)d2.len - hlen - QPP_TAG_LEN;
+                    Q.pn = ENC ? d2.pn : pn;
+                    Q.pn_off = Q.pn_len = 0;
+                    Q.fbm = 0;
+                    Q.mask = zero4();
+                    Q.nonce = zero4();
                     const LdsTe T2{sm.te, (t2 & 31) * 4};
                     const KeySlot *ks2 =
                         slots + __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
-                    gcm_finish<ENC, SUITE, BPL>(P, ks2, t2 & 3, scr2, T2, tag, got_tag);
+                    gcm_finish<ENC, SUITE, BPL>(Q, ks2, t2 & 3, T2, tag, got_tag);
+                    P = Q;
                 } else {
                     P.status = QPP_S_LENGTH;  // the item spans more than 4 GiB
                 }
@@ -1850,6 +1910,7 @@ int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *st
 // Workgroup sizes (tuned on MI355X, tools/sweep_wg.sh): GCM 1024 (one
 // persistent workgroup per CU, 4 waves per SIMD), ChaCha20-Poly1305 256.
 static const int kGcmWG = 1024;
+
 static const int kChachaWG = 256;
 
 // GCM blocks per lane per step (gcm_pad): 2 (r2i, same box: north star
@@ -1902,18 +1963,19 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     const uint32_t *d_items = plan ? plan->d_items : nullptr, *d_irange = plan ? plan->d_irange : nullptr;
     const uint32_t waves = plan ? qpp_internal_plan_max_items(n, kt->cap) : (n + 15) / 16;
     const int bpl_gcm = gcm_bpl_choice();
-#define QPP_LAUNCH_GCM_B(SUITE, BPLV)                                                          \
+#define QPP_LAUNCH_GCM_W(SUITE, BPLV, WGV)                                                     \
     do {                                                                                       \
-        const dim3 grid(gcm_grid(waves, kGcmWG / 64)), block(kGcmWG);                           \
+        const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
         if (enc)                                                                               \
-            hipLaunchKernelGGL((k_gcm<SUITE, true, kGcmWG, BPLV>), grid, block, 0, s,          \
+            hipLaunchKernelGGL((k_gcm<SUITE, true, WGV, BPLV>), grid, block, 0, s,             \
                                kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
                                d_items, d_irange);                                             \
         else                                                                                   \
-            hipLaunchKernelGGL((k_gcm<SUITE, false, kGcmWG, BPLV>), grid, block, 0, s,         \
+            hipLaunchKernelGGL((k_gcm<SUITE, false, WGV, BPLV>), grid, block, 0, s,            \
                                kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
                                d_items, d_irange);                                             \
     } while (0)
+#define QPP_LAUNCH_GCM_B(SUITE, BPLV) QPP_LAUNCH_GCM_W(SUITE, BPLV, kGcmWG)
 #define QPP_LAUNCH_GCM(SUITE)                                                                  \
     if (mask & (1u << SUITE)) {                                                                \
         if (bpl_gcm == 1) QPP_LAUNCH_GCM_B(SUITE, 1);                                           \
@@ -1934,6 +1996,7 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     }
 #undef QPP_LAUNCH_GCM
 #undef QPP_LAUNCH_GCM_B
+#undef QPP_LAUNCH_GCM_W
     return QPP_OK;
 }
 
