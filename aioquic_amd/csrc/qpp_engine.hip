@@ -1257,9 +1257,14 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
         sm.tick = 0u;
         sm.next = sb;
     }
+    if (threadIdx.x < WG / 64) sm.wslot[threadIdx.x] = kNoSlot;
     __syncthreads();
     QPP_PROBE_AT(0);  // prologue
 
+    // The wave's table entry stays held across its items while they run one
+    // slot (a single-key batch acquires it once; wslot / went in LDS, not
+    // SGPRs, which are spent): an item of the held slot skips the slot's
+    // suite lookup and the entry's acquisition.
 #pragma unroll 1
     for (;;) {
         uint32_t j = 0;
@@ -1370,7 +1375,9 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
             const uint32_t cur = wave_min_u32((last == kNoSlot || s > last) ? s : kNoSlot);
             if (cur == kNoSlot) break;
             last = cur;
-            const uint32_t suite = __builtin_amdgcn_readfirstlane(slots[cur].suite);
+            const uint32_t held = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
+            const uint32_t suite =
+                cur == held ? (uint32_t)SUITE : __builtin_amdgcn_readfirstlane(slots[cur].suite);
             if (suite > QPP_CHACHA20_POLY1305) {
                 // an empty slot: KeyUnavailableError (every suite's launch writes the same)
                 if (s == cur && (t & 3) == 0) {
@@ -1381,18 +1388,26 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
             }
             if (suite != SUITE) continue;  // another suite's launch
             QPP_PROBE_AT(1);
-            const uint32_t e = tab_acquire<WG>(sm, gtab, cur);
-            QPP_PROBE_AT(2);  // table entry
-            if (e == kNoSlot) continue;
-            if (lane_fresh() == 0) {
-                sm.wslot[wv] = cur;
-                sm.went[wv] = e;
+            if (cur != held) {
+                // release before acquiring: a wave never waits holding an entry
+                if (held != kNoSlot) {
+                    tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.went[wv]));
+                    if (lane_fresh() == 0) *(volatile uint32_t *)&sm.wslot[wv] = kNoSlot;
+                }
+                const uint32_t e = tab_acquire<WG>(sm, gtab, cur);
+                if (e == kNoSlot) continue;
+                if (lane_fresh() == 0) {
+                    *(volatile uint32_t *)&sm.wslot[wv] = cur;
+                    *(volatile uint32_t *)&sm.went[wv] = e;
+                }
             }
+            QPP_PROBE_AT(2);  // table entry
             run_slot(cur);
-            tab_release<WG>(sm, e);
             QPP_PROBE_AT(8);
         }
     }
+    if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]) != kNoSlot)
+        tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.went[wv]));
     QPP_PROBE_AT(9);
 }
 
