@@ -576,6 +576,20 @@ __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, con
     // every step wait for all of its outstanding table lookups
     const uint32_t t4 = G.t4();
     const u32x4 tiny_in = tiny ? ld_part(P.src, rlen) : zero4();
+    const int q = pad + za;  // sequence position of CT block 0
+    const uint32_t cin = ioff + (uint32_t)hlen, cout = ooff + (uint32_t)hlen;
+    // buffer offset of CT block i's input (or out of range)
+    auto ct_load = [&](int i) -> uint32_t {
+        if (i < 0 || 16 * i >= clen) return kOob;
+        return cin + (uint32_t)(ENC ? min(16 * i, clen - 16) : 16 * i);
+    };
+    // BPL = 2: the first step's two input blocks, requested before the
+    // associated data and the counter cache so that their latency overlaps them
+    u32x4 nxt0 = {0, 0, 0, 0}, nxt1 = {0, 0, 0, 0};
+    if constexpr (BPL == 2) {
+        nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(sub - q), 0, 0);
+        nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(sub - q + 4), 0, 0);
+    }
 
     // fold the associated data (unmasked for unprotect) into Z
     u32x4 z = {0, 0, 0, 0};
@@ -604,10 +618,8 @@ __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, con
     // in its first step's only block); BPL = 2: Z may sit at the second block
     // of a lane's first step, so it enters through that step's input (step2)
     u32x4 acc = (BPL == 1 && za && sub == pad) ? z : u32x4{0, 0, 0, 0};
-    const int q = pad + za;  // sequence position of CT block 0
     const CtrCache cc = ctr_cache(P.nonce, rk, T);
     const uint32_t lens_h = bswap((uint32_t)hlen * 8u);
-    const uint32_t cin = ioff + (uint32_t)hlen, cout = ooff + (uint32_t)hlen;
 
     // The last step: lane j closes its Horner chain with H^(4-j) (the slot's
     // global table of power 3 - j), and the lengths block's lane (lane 3, the
@@ -705,12 +717,6 @@ __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, con
         if (!last) acc = ghash_mul_h4(acc, G.lds, t4);
         else close(ks1);
     };
-    // buffer offset of CT block i's input (or out of range)
-    auto ct_load = [&](int i) -> uint32_t {
-        if (i < 0 || 16 * i >= clen) return kOob;
-        return cin + (uint32_t)(ENC ? min(16 * i, clen - 16) : 16 * i);
-    };
-
     got_tag = u32x4{0, 0, 0, 0};
     if constexpr (BPL == 2) {
         if (tiny) {
@@ -719,10 +725,9 @@ __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, con
             step2(sub - q, true, st, st, std::true_type{});
         } else {
             int i = sub - q;
-            // register prefetch of both blocks, one step ahead; on the last
-            // step the first of them is the received tag (unprotect)
-            u32x4 nxt0 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i), 0, 0);
-            u32x4 nxt1 = __builtin_amdgcn_raw_buffer_load_b128(B.in, (int)ct_load(i + 4), 0, 0);
+            // register prefetch of both blocks, one step ahead (the first
+            // step's since the top); on the last step the first of them is the
+            // received tag (unprotect)
             auto one2 = [&](int k, auto first_c) {
                 const u32x4 raw0 = nxt0, raw1 = nxt1;
                 const uint32_t l0 = (!ENC && k == 1) ? cin + (uint32_t)clen : ct_load(i + 8);
