@@ -1121,9 +1121,13 @@ __device__ __forceinline__ void write_result(qpp_result *res, uint32_t p, int su
 // it waits for one to come free.  A share of a bucketed batch walks its
 // slots in order, so the 16 waves hold one or two slots at a time.
 constexpr int kTabEntries = 4;
+// Two 512-thread workgroups per CU (launch_packets: small single-key
+// launches) hold one table entry each.
+template <int WG>
+constexpr int gcm_tab_entries() { return WG == 512 ? 1 : kTabEntries; }
 static_assert(kGhLdsEntry % 1024 == 0, "LDS-DMA pieces of 1 KiB");
 
-template <int WG, int NE = kTabEntries>
+template <int WG, int NE = gcm_tab_entries<WG>()>
 struct __attribute__((aligned(16))) GcmSmem {
     // GHASH table entries first (LDS offset 0: the entry's offset rides in
     // the 5-bit window address), then the AES image, whose base stays within
@@ -1160,7 +1164,7 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
             int hit = -1, vic = -1;
             uint32_t best = 0xffffffffu;
 #pragma unroll
-            for (int i = 0; i < kTabEntries; ++i) {
+            for (int i = 0; i < gcm_tab_entries<WG>(); ++i) {
                 const uint32_t s = ((volatile uint32_t *)sm.eslot)[i];
                 const uint32_t r = ((volatile uint32_t *)sm.eref)[i];
                 const uint32_t u = ((volatile uint32_t *)sm.eused)[i];
@@ -1222,7 +1226,7 @@ __device__ __forceinline__ void tab_release(GcmSmem<WG> &sm, uint32_t e)
 }
 
 template <int SUITE, bool ENC, int WG, int BPL>
-__global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_gcm(const KeySlot *__restrict__ slots,
                                               const uint8_t *__restrict__ gtab, uint32_t cap,
                                               const qpp_desc *__restrict__ desc, uint32_t n,
                                               const uint8_t *gin, uint8_t *gout,
@@ -1251,7 +1255,7 @@ __global__ __launch_bounds__(WG, 1) void k_gcm(const KeySlot *__restrict__ slots
     // loop is spilled to scratch (HBM traffic and latency).
     auto tid_now = [&]() -> uint32_t { return (wv << 6) | lane_fresh(); };
     load_te<WG>(sm.te);
-    if (threadIdx.x < kTabEntries) {
+    if (threadIdx.x < gcm_tab_entries<WG>()) {
         sm.eslot[threadIdx.x] = kNoSlot;
         sm.eref[threadIdx.x] = 0u;
         sm.eready[threadIdx.x] = 0u;
@@ -1946,10 +1950,7 @@ static int gcm_bpl_choice()
     return b;
 }
 
-// Persistent GCM grid: one workgroup per CU (the kernel's LDS admits no
-// second), fewer when the batch has fewer than a workgroup's worth of items
-// per CU.
-static uint32_t gcm_grid(uint32_t items, uint32_t waves_per_wg)
+static uint32_t cu_count()
 {
     static int cus[64];
     int dev = 0;
@@ -1963,8 +1964,27 @@ static uint32_t gcm_grid(uint32_t items, uint32_t waves_per_wg)
         }
         cus[dev] = c;
     }
+    return (uint32_t)cus[dev];
+}
+
+// Persistent GCM grid: one 1024-thread workgroup per CU (or two of 512),
+// fewer when the batch has fewer than a workgroup's worth of items per CU.
+static uint32_t gcm_grid(uint32_t items, uint32_t waves_per_wg)
+{
     const uint32_t need = (items + waves_per_wg - 1) / waves_per_wg;
-    return need < (uint32_t)cus[dev] ? (need ? need : 1u) : (uint32_t)cus[dev];
+    const uint32_t cap = cu_count() * (waves_per_wg == 8 ? 2u : 1u);
+    return need < cap ? (need ? need : 1u) : cap;
+}
+
+// GCM launch shape.  Two 512-thread workgroups per CU run the step loop's
+// lookups ~9 % faster than one of 1024 (profiles/r3u_probe_wg*.txt), but the
+// two workgroups sharing a CU do not progress at the same rate, so over many
+// items per wave one ends well before the other; and each holds one GHASH
+// table entry.  So: two per CU when the table holds one key of the suite and
+// the launch has at most one item per wave.
+static bool gcm_two_wg(const qpp_keytab *kt, uint32_t suite, uint32_t items)
+{
+    return kt->n_suite[suite] == 1 && items <= cu_count() * 16u;  // 2 workgroups x 8 waves per CU
 }
 
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
@@ -1995,7 +2015,11 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
                                kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
                                d_items, d_irange);                                             \
     } while (0)
-#define QPP_LAUNCH_GCM_B(SUITE, BPLV) QPP_LAUNCH_GCM_W(SUITE, BPLV, kGcmWG)
+#define QPP_LAUNCH_GCM_B(SUITE, BPLV)                                                          \
+    do {                                                                                       \
+        if (BPLV == 2 && gcm_two_wg(kt, SUITE, waves)) QPP_LAUNCH_GCM_W(SUITE, BPLV, 512);       \
+        else QPP_LAUNCH_GCM_W(SUITE, BPLV, kGcmWG);                                             \
+    } while (0)
 #define QPP_LAUNCH_GCM(SUITE)                                                                  \
     if (mask & (1u << SUITE)) {                                                                \
         if (bpl_gcm == 1) QPP_LAUNCH_GCM_B(SUITE, 1);                                           \

@@ -463,6 +463,94 @@ static void run_step(const char *name, int dyn, const uint32_t *rk, const uint8_
     fflush(stdout);
 }
 
+
+// k_step with the kernel's memory side: per lane-step two 16-byte loads one
+// step ahead and two 16-byte stores, a quad covering 128 contiguous bytes
+// (16 packets of 1200 bytes per wave, each quad walking its packet).
+template <int WG>
+__global__ __launch_bounds__(WG) void k_stepm(const uint32_t *rk_g, const uint8_t *gt_g, int steps,
+                                              const uint8_t *gin, uint8_t *gout, uint32_t *out)
+{
+    __shared__ SmemStep sm;
+    fill_te<WG>(sm.te);
+    for (int i = threadIdx.x; i < kGh5Bytes / 16; i += WG) ((u32x4 *)sm.gh)[i] = ((const u32x4 *)gt_g)[i];
+    __syncthreads();
+    uint32_t rk[44];
+#pragma unroll
+    for (int i = 0; i < 44; ++i) rk[i] = __builtin_amdgcn_readfirstlane(rk_g[i]);
+    const LdsTe T{sm.te, (uint32_t)(threadIdx.x & 31) * 4};
+    u32x4 acc = u32x4{threadIdx.x, blockIdx.x, 0u, 0u};
+    const CtrCache cc = ctr_cache(u32x4{blockIdx.x, threadIdx.x, 7u, 0}, rk, T);
+    // packet of this quad: 1200-byte slots, 11-byte header
+    const uint32_t pk = (blockIdx.x * WG + threadIdx.x) >> 2, j = threadIdx.x & 3;
+    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)gin, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)gout, 0, 0x7fffffff, 0x00020000);
+    const uint32_t base = pk * 1200u + 11u;
+    auto off = [&](int k, int h) -> uint32_t { return base + (uint32_t)(((8 * k + 4 * h + (int)j) % 72) * 16); };
+    u32x4 n0 = __builtin_amdgcn_raw_buffer_load_b128(ri, (int)off(0, 0), 0, 0);
+    u32x4 n1 = __builtin_amdgcn_raw_buffer_load_b128(ri, (int)off(0, 1), 0, 0);
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < steps; ++k) {
+        const u32x4 r0 = n0, r1 = n1;
+        n0 = __builtin_amdgcn_raw_buffer_load_b128(ri, (int)off(k + 1, 0), 0, 0);
+        n1 = __builtin_amdgcn_raw_buffer_load_b128(ri, (int)off(k + 1, 1), 0, 0);
+        u32x4 o0, o1;
+        const uint32_t cb = (uint32_t)(k & 127) ^ (acc.x & 1);
+        aes_ctr2<10>(cc, 2 * cb, 2 * cb + 1, rk, T, o0, o1);
+        o0 ^= r0;
+        o1 ^= r1;
+        __builtin_amdgcn_raw_buffer_store_b128(o0, ro, (int)off(k, 0), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(o1, ro, (int)off(k, 1), 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = ghash_mul_h4(acc ^ o0, sm.gh, 0) ^ o1;
+        acc = ghash_mul_h4(acc, sm.gh, 0);
+    }
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {
+        g_clk[blockIdx.x * 4 + 0] = c0;
+        g_clk[blockIdx.x * 4 + 1] = c1;
+        g_clk[blockIdx.x * 4 + 2] = t0;
+        g_clk[blockIdx.x * 4 + 3] = t1;
+    }
+    out[blockIdx.x * WG + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+template <int WG>
+static void run_stepm(const char *name, int dyn, const uint32_t *rk, const uint8_t *gt, uint32_t *out,
+                      const uint8_t *gin, uint8_t *gout)
+{
+    const int blocks = 2048 * 1024 / WG, steps = 32;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int w = 0; w < 3; ++w)
+        hipLaunchKernelGGL((k_stepm<WG>), dim3(blocks), dim3(WG), dyn, 0, rk, gt, steps, gin, gout, out);
+    const int reps = 5;
+    (void)hipEventRecord(a, 0);
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((k_stepm<WG>), dim3(blocks), dim3(WG), dyn, 0, rk, gt, steps, gin, gout, out);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    ms /= reps;
+    std::vector<unsigned long long> clk(4096 * 4);
+    (void)hipMemcpyFromSymbol(clk.data(), HIP_SYMBOL(g_clk), clk.size() * 8, 0, hipMemcpyDeviceToHost);
+    double cyc = 0, tick = 0;
+    const int nb = blocks < 4096 ? blocks : 4096;
+    for (int i = 0; i < nb; ++i) {
+        cyc += (double)(clk[i * 4 + 1] - clk[i * 4 + 0]);
+        tick += (double)(clk[i * 4 + 3] - clk[i * 4 + 2]);
+    }
+    const double mhz = cyc / (tick / 100.0);
+    const double cu_cyc = ms * 1e-3 * mhz * 1e6 * 256 / ((double)blocks * WG * steps * 2);
+    const double f = (133.0 * 2 + 26.0 * 2) / 64;
+    printf("%-40s %8.3f ms  clock %5.0f MHz  %6.2f CU-cycles/block  LDS floor %.2f frac %.2f\n", name, ms, mhz, cu_cyc,
+           f, f / cu_cyc);
+    fflush(stdout);
+}
+
 // LDS-array cycles per block per wave-instruction model (MI355X_MICROARCH.md sec. LDS):
 // ds_read_b32 = 2 cycles, ds_read_b128 = 4 cycles per 64 lanes
 static double lds_model(int mode)
@@ -539,6 +627,31 @@ int main()
         uint32_t hb = 0;
         (void)hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
         printf("check aes_ctr2s == aes_ctr2 == aes_ctr: %u mismatching lanes of %d\n", hb, 64 * 1024);
+    }
+    if (getenv("MB_STEPM_ONLY")) {
+        // 2048 x 1024 lanes / 4 = 512 Ki packets of 1200 bytes
+        uint8_t *gin, *gout;
+        (void)hipMalloc(&gin, (size_t)512 * 1024 * 1200 + 4096);
+        (void)hipMalloc(&gout, (size_t)512 * 1024 * 1200 + 4096);
+        (void)hipMemset(gin, 7, (size_t)512 * 1024 * 1200 + 4096);
+        for (int rep = 0; rep < 2; ++rep) {
+            run_step<1024>("step 1x1024 (dyn)", 8 * 1024, rk, gt, out);
+            run_step<512>("step 2x512", 0, rk, gt, out);
+            run_stepm<1024>("step+mem 1x1024 (dyn)", 8 * 1024, rk, gt, out, gin, gout);
+            run_stepm<512>("step+mem 2x512", 0, rk, gt, out, gin, gout);
+        }
+        return 0;
+    }
+    if (getenv("MB_OFF2_ONLY")) {
+        // two 512-thread workgroups per CU with the image at the offsets the
+        // engine's layouts put it (after 1 or 4 GHASH entries), against 0
+        for (int rep = 0; rep < 2; ++rep) {
+            run_occ<512, 0>("2x512, te at 0", 0, rk, out);
+            run_occ<512, 14336>("2x512, te at 14K (1 entry first)", 0, rk, out);
+            run_occ<1024, 57344>("1x1024, te at 56K (engine)", 0, rk, out);
+            run_occ<512, 0>("2x512, te at 0, dyn 14K", 14336, rk, out);
+        }
+        return 0;
     }
     if (getenv("MB_STEP_ONLY")) {
         for (int rep = 0; rep < 2; ++rep) {
