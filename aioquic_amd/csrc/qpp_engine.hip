@@ -794,7 +794,8 @@ __device__ __forceinline__ void gcm_finish(Pkt &P, const KeySlot *ks, int sub, c
             P.pn_len = (int)(b0 & 3) + 1;
             P.pn_off = P.hlen - P.pn_len;
             P.fbm = first_byte_mask(b0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // (the tag went out by a flat store: both counters)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             const __amdgpu_buffer_rsrc_t r =
                 __builtin_amdgcn_make_buffer_rsrc((void *)(P.dst + P.hlen), 0, 64, 0x00020000);
             const u32x4 smp = __builtin_amdgcn_raw_buffer_load_b128(r, 4 - P.pn_len, 0, 1);
