@@ -143,15 +143,39 @@ def _random_batch(rng, n, n_slots, recs, *, max_payload=1400, pn_lens=(1, 2, 3, 
 
 @pytest.mark.parametrize("bpl", ["1", "2"], ids=["gcm-bpl1", "gcm-bpl2"])
 @pytest.mark.parametrize("align", [1, 16, -16], ids=["align1", "align16", "payload16"])
-def test_random_batch_vs_oracle(oracle, L, engine_cls, align, bpl, monkeypatch):
+def test_random_batch_vs_oracle(oracle, L, engine_cls, align, bpl):
     """Ragged, misaligned packets of all suites and mixed key slots vs the oracle,
-    under both GCM step forms (QPP_GCM_BPL: one or two blocks per lane a step;
-    the library reads the switch at every launch); align < 0: payloads on
-    multiples of -align (layout_packets(payload_align=...))."""
-    from aioquic_amd.batch import layout_packets
+    under both GCM step forms (QPP_GCM_BPL: one or two blocks per lane a step);
+    align < 0: payloads on multiples of -align (layout_packets(payload_align=...)).
+    The library reads QPP_GCM_BPL once per process, so the one-block form runs
+    in a child process started with QPP_GCM_BPL=1."""
+    if bpl == "1":
+        import subprocess
+        import sys
 
-    monkeypatch.setenv("QPP_GCM_BPL", bpl)
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        code = ("import sys; sys.path.insert(0, %r); from tests.test_gpu_parity import random_batch_check; "
+                "random_batch_check(%d, 'QPP_GCM_BPL=1')" % (root, align))
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, QPP_GCM_BPL="1"),
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+        assert "random_batch_check ok QPP_GCM_BPL=1" in r.stdout
+        return
+    random_batch_check(align, "", oracle, L, engine_cls)
 
+
+def random_batch_check(align, tag, oracle=None, L=None, engine_cls=None):
+    """Body of test_random_batch_vs_oracle (also run in a child process)."""
+    from aioquic_amd.batch import PacketEngine, layout_packets
+
+    if oracle is None:
+        from oracle import oracle as orc
+
+        orc.lib()
+        oracle = orc
+    if L is None:
+        from aioquic_amd import layout as L
+    engine_cls = engine_cls or PacketEngine
     rng = np.random.default_rng(0x9001 + abs(align))
     n_slots = 24
     recs = _keys(rng, n_slots)
@@ -188,6 +212,8 @@ def test_random_batch_vs_oracle(oracle, L, engine_cls, align, bpl, monkeypatch):
         if not quirk[i]:
             assert u_g[o : o + n_].tobytes() == headers[i] + payloads[i]
             assert np.array_equal(u_g[o : o + n_], u_o[o : o + n_])
+    if tag:
+        print("random_batch_check ok", tag)
 
 
 def test_tamper_and_edge_status(oracle, L, engine_cls):
