@@ -1385,6 +1385,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             const uint32_t cur = wave_min_u32((last == kNoSlot || s > last) ? s : kNoSlot);
             if (cur == kNoSlot) break;
             last = cur;
+            // no packet of the item on a later slot: this slot is its last, so
+            // the loop ends after it without reading the descriptors again
+            // (a load there would wait behind the item's stores)
+            const bool final_slot = __builtin_amdgcn_ballot_w64(s != kNoSlot && s > cur) == 0;
             const uint32_t held = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
             const uint32_t suite =
                 cur == held ? (uint32_t)SUITE : __builtin_amdgcn_readfirstlane(slots[cur].suite);
@@ -1414,6 +1418,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             QPP_PROBE_AT(2);  // table entry
             run_slot(cur);
             QPP_PROBE_AT(8);
+            if (final_slot) break;
         }
     }
     if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]) != kNoSlot)
