@@ -459,6 +459,20 @@ __device__ __forceinline__ Pkt unpark(const uint8_t *scr, const uint8_t *src, ui
 // the workgroup's LDS table entries, the few other powers from the slot's
 // tables in global memory (gcm_packet).  The wave's slot and entry live in
 // LDS, re-read where needed rather than kept in SGPRs.
+// Workgroup-shared bookkeeping words in LDS, read and written as relaxed
+// workgroup-scope atomics: volatile accesses through generic pointers compile
+// to flat instructions, and a flat load waits for the vector memory counter
+// too (behind the item's outstanding stores), where an LDS load waits only
+// for LDS.
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 struct GhashTabs {
     const uint8_t *lds;     // LDS table entries
     const uint8_t *gtab;    // every slot's tables, global memory
@@ -466,12 +480,12 @@ struct GhashTabs {
     const uint32_t *went;   // LDS: the wave's table entry
     __device__ __forceinline__ uint32_t t4() const
     {
-        return __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)went) * (uint32_t)kGhLdsEntry;
+        return __builtin_amdgcn_readfirstlane(lds_ld(went)) * (uint32_t)kGhLdsEntry;
     }
     // the slot's table of H^(pw + 1) in global memory
     __device__ __forceinline__ const uint8_t *global(uint32_t pw) const
     {
-        const uint32_t s = __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)wslot);
+        const uint32_t s = __builtin_amdgcn_readfirstlane(lds_ld(wslot));
         return gtab + (size_t)s * kGhashTabBytes + pw * (uint32_t)kGhashPowBytes;
     }
 };
@@ -1166,9 +1180,9 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
             uint32_t best = 0xffffffffu;
 #pragma unroll
             for (int i = 0; i < gcm_tab_entries<WG>(); ++i) {
-                const uint32_t s = ((volatile uint32_t *)sm.eslot)[i];
-                const uint32_t r = ((volatile uint32_t *)sm.eref)[i];
-                const uint32_t u = ((volatile uint32_t *)sm.eused)[i];
+                const uint32_t s = lds_ld(&sm.eslot[i]);
+                const uint32_t r = lds_ld(&sm.eref[i]);
+                const uint32_t u = lds_ld(&sm.eused[i]);
                 if (s == cur) hit = i;
                 else if (r == 0u && u < best) {
                     best = u;
@@ -1178,15 +1192,15 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
             if (hit < 0 && vic >= 0) {
                 hit = vic;
                 ld = 1;
-                ((volatile uint32_t *)sm.eslot)[vic] = cur;
-                ((volatile uint32_t *)sm.eready)[vic] = 0u;
+                lds_st(&sm.eslot[vic], cur);
+                lds_st(&sm.eready[vic], 0u);
             }
             if (hit >= 0) {
                 got = (uint32_t)hit;
                 atomicAdd(&sm.eref[hit], 1u);  // atomic: releases decrement without the lock
-                const uint32_t t = ((volatile uint32_t *)&sm.tick)[0] + 1u;
-                ((volatile uint32_t *)&sm.tick)[0] = t;
-                ((volatile uint32_t *)sm.eused)[hit] = t;
+                const uint32_t t = lds_ld(&sm.tick) + 1u;
+                lds_st(&sm.tick, t);
+                lds_st(&sm.eused[hit], t);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // bookkeeping before the unlock
             atomicExch(&sm.lock, 0u);
@@ -1209,11 +1223,11 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
             __builtin_amdgcn_global_load_lds((gptr_t)(src + c * 1024 + l * 16), (lptr_t)(sm.h4[e] + c * 1024),
                                              16, 0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane_fresh() == 0) ((volatile uint32_t *)sm.eready)[e] = 1u;
+        if (lane_fresh() == 0) lds_st(&sm.eready[e], 1u);
     } else {
 #pragma unroll 1
         for (int spin = 0; spin < (1 << 22); ++spin) {
-            if (__builtin_amdgcn_readfirstlane(((volatile uint32_t *)sm.eready)[e])) break;
+            if (__builtin_amdgcn_readfirstlane(lds_ld(&sm.eready[e]))) break;
             __builtin_amdgcn_s_sleep(2);
         }
     }
@@ -1362,7 +1376,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     Q.nonce = zero4();
                     const LdsTe T2{sm.te, (t2 & 31) * 4};
                     const KeySlot *ks2 =
-                        slots + __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
+                        slots + __builtin_amdgcn_readfirstlane(lds_ld(&sm.wslot[wv]));
                     gcm_finish<ENC, SUITE, BPL>(Q, ks2, t2 & 3, T2, tag, got_tag);
                     P = Q;
                 } else {
@@ -1389,7 +1403,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             // the loop ends after it without reading the descriptors again
             // (a load there would wait behind the item's stores)
             const bool final_slot = __builtin_amdgcn_ballot_w64(s != kNoSlot && s > cur) == 0;
-            const uint32_t held = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]);
+            const uint32_t held = __builtin_amdgcn_readfirstlane(lds_ld(&sm.wslot[wv]));
             const uint32_t suite =
                 cur == held ? (uint32_t)SUITE : __builtin_amdgcn_readfirstlane(slots[cur].suite);
             if (suite > QPP_CHACHA20_POLY1305) {
@@ -1405,14 +1419,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             if (cur != held) {
                 // release before acquiring: a wave never waits holding an entry
                 if (held != kNoSlot) {
-                    tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.went[wv]));
-                    if (lane_fresh() == 0) *(volatile uint32_t *)&sm.wslot[wv] = kNoSlot;
+                    tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(lds_ld(&sm.went[wv])));
+                    if (lane_fresh() == 0) lds_st(&sm.wslot[wv], kNoSlot);
                 }
                 const uint32_t e = tab_acquire<WG>(sm, gtab, cur);
                 if (e == kNoSlot) continue;
                 if (lane_fresh() == 0) {
-                    *(volatile uint32_t *)&sm.wslot[wv] = cur;
-                    *(volatile uint32_t *)&sm.went[wv] = e;
+                    lds_st(&sm.wslot[wv], cur);
+                    lds_st(&sm.went[wv], e);
                 }
             }
             QPP_PROBE_AT(2);  // table entry
@@ -1421,8 +1435,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             if (final_slot) break;
         }
     }
-    if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.wslot[wv]) != kNoSlot)
-        tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&sm.went[wv]));
+    if (__builtin_amdgcn_readfirstlane(lds_ld(&sm.wslot[wv])) != kNoSlot)
+        tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(lds_ld(&sm.went[wv])));
     QPP_PROBE_AT(9);
 }
 
