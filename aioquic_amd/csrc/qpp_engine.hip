@@ -29,15 +29,16 @@ namespace qpp {
 
 __constant__ AesTables c_aes = kAesTables;
 
-// GCM: one workgroup per CU shares one 64 KiB AES image and one 32 KiB GHASH
-// table set; the workgroup size sets the waves per SIMD (and so the VGPR
-// budget): 512 -> 2 (256 VGPRs), 768 -> 3 (168), 1024 -> 4 (128).
+// GCM: a workgroup shares one 64 KiB AES image and its GHASH table entries;
+// one 1024-thread workgroup per CU, or two of 512 (launch_packets), at 4
+// waves per SIMD (128 VGPRs) either way.
 // ChaCha20-Poly1305 needs no tables.  4 lanes per packet in every case.
 constexpr int kSetupWG = 256;
-// Per-packet LDS scratch: [0, 32) ct[0..32) (+ tag) for the protect HP
-// sample; [32, 48) tiny-input staging, then the partial tail block; [48, 64)
-// E_K(J0); [64, 96) the parked packet view (GCM step loop); [96, 112) input
-// bytes [0, 16) (the first header block) for the header write.
+// Per-packet LDS scratch of the ChaCha20-Poly1305 kernel (the GCM kernel
+// keeps nothing of a packet in LDS): [0, 32) ct[0..32) (+ tag) for the
+// protect HP sample; [48, 64) the Poly1305 one-time key's s half; [64, 96)
+// the parked packet view; [96, 112) input bytes [0, 16) (the first header
+// block) for the header write.
 constexpr int kScratch = 112;
 constexpr int kScrEj0 = 48, kScrPark = 64, kScrHdr = 96;
 constexpr uint32_t kNoSlot = 0xffffffffu;
