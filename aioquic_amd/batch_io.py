@@ -29,6 +29,11 @@ step (quic/connection.py:905-947, CryptoPair.decrypt_packet, crypto.py:184-192).
   Outcomes are (plain_header, payload, packet_number) tuples or the exception
   the reference raises: KeyUnavailableError -> "key_unavailable" drop,
   CryptoError -> "payload_decrypt_error" drop (connection.py:911-947).
+  Items may name their connection and its reserved-bit mask (receive_datagram's
+  check after the decrypt, connection.py:949-960): a packet that authenticates
+  with a reserved bit set gives ReservedBitsError, closes its connection and
+  leaves the expected number alone; every later packet of a closed connection
+  gives ConnectionClosedError without touching any state (:756-757).
 """
 
 from __future__ import annotations
@@ -45,7 +50,21 @@ from ._crypto import CryptoError, KeyTable, protect_list, unprotect_list, unprot
 from .crypto import CryptoContext, CryptoPair, KeyUnavailableError, next_key_phase
 from .packet import decode_packet_number
 
-__all__ = ["SendBatch", "ReceiveBatch", "KeySlots"]
+__all__ = ["SendBatch", "ReceiveBatch", "KeySlots", "ReservedBitsError", "ConnectionClosedError"]
+
+# host-side statuses of the C receive walks (_crypto_ext.c WALK_S_*)
+_S_RESERVED, _S_CLOSED = 0x101, 0x102
+_NO_CONN = 0xFFFFFFFF
+
+
+class ReservedBitsError(Exception):
+    """The packet authenticated but carries a reserved header bit: the
+    reference closes the connection (PROTOCOL_VIOLATION, connection.py:949-960)."""
+
+
+class ConnectionClosedError(Exception):
+    """The packet's connection was closed by an earlier packet of the batch;
+    the reference ignores it (connection.py:756-757)."""
 
 
 class KeySlots:
@@ -163,6 +182,10 @@ def default_slots() -> KeySlots:
 
 
 def _raise_status(status: int) -> Exception:
+    if status == _S_RESERVED:
+        return ReservedBitsError("Reserved bits must be zero")
+    if status == _S_CLOSED:
+        return ConnectionClosedError("Connection is closed")
     if status == L.S_DECRYPT:
         return CryptoError("Payload decryption failed")
     if status == L.S_NO_KEY:
@@ -285,16 +308,21 @@ class ReceiveBatch:
         self._offs: list = []
         self._spaces: list = []
         self._track: list = []
+        self._conns: list = []  # connection key per item (None: none)
+        self._rsv: list = []    # reserved-bit mask per item (0: no check)
+        self._closed: set = set()  # connections closed by the walk so far
         self.launches = 0
 
     def __len__(self) -> int:
         return len(self._pairs)
 
     def add(self, pair: CryptoPair, packet: bytes, encrypted_offset: int,
-            expected_packet_number: Optional[int] = None, space=None) -> int:
+            expected_packet_number: Optional[int] = None, space=None, conn=None, reserved_mask: int = 0) -> int:
         """Queue one packet.  Give either an explicit expected packet number or
         a packet-number space (any object with .expected_packet_number), which
-        run() then advances as connection.py:984-985 does."""
+        run() then advances as connection.py:984-985 does.  `conn` (any
+        object, by identity) and `reserved_mask` (0x18 for a short header,
+        0x0C for a long one) add receive_datagram's reserved-bit close."""
         if (expected_packet_number is None) == (space is None):
             raise ValueError("give exactly one of expected_packet_number / space")
         track = space is not None
@@ -303,9 +331,12 @@ class ReceiveBatch:
         self._offs.append(int(encrypted_offset))
         self._spaces.append(space if track else _Space(int(expected_packet_number)))
         self._track.append(track)
+        self._conns.append(conn)
+        self._rsv.append(int(reserved_mask) & 0xFF)
         return len(self._pairs) - 1
 
-    def _extend(self, pairs: list, packets: list, offs: list, spaces: list) -> None:
+    def _extend(self, pairs: list, packets: list, offs: list, spaces: list, conns: Optional[list] = None,
+                rsv: int = 0) -> None:
         """add() for many packets at once, each with a tracked space (the
         batched receive walk's form: packets are bytes, no copies)."""
         self._pairs += pairs
@@ -313,44 +344,49 @@ class ReceiveBatch:
         self._offs += offs
         self._spaces += spaces
         self._track += [True] * len(pairs)
+        self._conns += conns if conns is not None else [None] * len(pairs)
+        self._rsv += [rsv] * len(pairs)
 
     def _fast_round(self, outcome: list) -> list:
         """The first round in C (_crypto.unprotect_walk): one launch and the
         in-order walk for every packet whose outcome no state change of this
         round can alter; returns the deferred items (in order) for the
-        general rounds of run()."""
-        pairs, spaces, offs, track = self._pairs, self._spaces, self._offs, self._track
+        general rounds of run().  Every item goes to the walk, those without a
+        receive key or with a packet-number offset past the header limit too
+        (the walk fails them by their slot and offset), so a closed
+        connection's packets come back closed in order."""
+        pairs, spaces, offs, track, conns = self._pairs, self._spaces, self._offs, self._track, self._conns
         n = len(pairs)
-        launch = [i for i in range(n) if pairs[i].recv.aead is not None and offs[i] <= L.MAX_HDR]
-        if len(launch) != n:
-            for i in set(range(n)).difference(launch):
-                outcome[i] = (KeyUnavailableError("Decryption key is not available") if pairs[i].recv.aead is None
-                              else CryptoError("Invalid payload length"))
-        if not launch:
+        if not n:
             return []
-        # pairs and spaces by identity, each resolved once
+        # pairs, spaces and connections by identity, each resolved once
         pix: dict = {}
         six: dict = {}
-        p_of = [pix.setdefault(id(pairs[i]), len(pix)) for i in launch]
-        s_of = [six.setdefault(id(spaces[i]), len(six)) for i in launch]
+        cix: dict = {}
+        p_of = [pix.setdefault(id(p), len(pix)) for p in pairs]
+        s_of = [six.setdefault(id(sp), len(six)) for sp in spaces]
+        c_of = [_NO_CONN if c is None else cix.setdefault(id(c), len(cix)) for c in conns]
         upairs = [None] * len(pix)
-        for i, k in zip(launch, p_of):
-            upairs[k] = pairs[i]
+        for p, k in zip(pairs, p_of):
+            upairs[k] = p
         uspaces = [None] * len(six)
-        for i, k in zip(launch, s_of):
-            uspaces[k] = spaces[i]
-        keys = _KeyRefs()
-        prefs = [keys.ref(p.recv.aead, p.recv.hp, p.recv.key_phase) for p in upairs]
-        pslot = np.asarray(self.slots.assign(keys.triples), dtype=np.uint32)[np.asarray(prefs, np.int64)]
+        for sp, k in zip(spaces, s_of):
+            uspaces[k] = sp
+        keyed = [k for k, p in enumerate(upairs) if p.recv.aead is not None]
+        pslot = np.full(len(upairs), 0xFFFFFFFF, np.uint32)
+        if keyed:
+            keys = _KeyRefs()
+            prefs = [keys.ref(upairs[k].recv.aead, upairs[k].recv.hp, upairs[k].recv.key_phase) for k in keyed]
+            pslot[keyed] = np.asarray(self.slots.assign(keys.triples), dtype=np.uint32)[np.asarray(prefs, np.int64)]
         p_arr = np.asarray(p_of, dtype=np.uint32)
         s_arr = np.asarray(s_of, dtype=np.uint32)
         sexp = np.asarray([sp.expected_packet_number & 0xFFFFFFFFFFFFFFFF for sp in uspaces], dtype=np.uint64)
-        outs, res, deferred, sexp2 = unprotect_walk(
-            self.slots.table, pslot[p_arr].tobytes(), sexp[s_arr].tobytes(),
-            [self._packets[i] for i in launch] if len(launch) != n else self._packets,
-            np.asarray([min(offs[i], 0xFFFF) for i in launch], np.uint32).tobytes(),
-            p_arr.tobytes(), s_arr.tobytes(), np.asarray([track[i] for i in launch], np.uint8).tobytes(),
-            sexp.tobytes(), len(upairs))
+        outs, res, deferred, sexp2, closed = unprotect_walk(
+            self.slots.table, pslot[p_arr].tobytes(), sexp[s_arr].tobytes(), self._packets,
+            np.asarray([min(o, 0xFFFF) for o in offs], np.uint32).tobytes(),
+            p_arr.tobytes(), s_arr.tobytes(), np.asarray(track, np.uint8).tobytes(),
+            sexp.tobytes(), len(upairs), np.asarray(c_of, np.uint32).tobytes(),
+            np.asarray(self._rsv, np.uint8).tobytes(), bytes(len(cix)))
         self.launches += 1
         # outcomes: successes come as (header, payload, pn); failures by status
         st = np.frombuffer(res, dtype=L.RESULT)["status"]
@@ -359,16 +395,18 @@ class ReceiveBatch:
         for k in fail.tolist():
             if k not in dset:
                 outs[k] = _raise_status(int(st[k]))
-        if len(launch) == n:
-            outcome[:] = outs
-        else:
-            for k, i in enumerate(launch):
-                outcome[i] = outs[k]
+        outcome[:] = outs
         # the spaces' expected numbers after the walk (only tracked spaces move)
         new = np.frombuffer(sexp2, dtype=np.uint64)
         for k in np.flatnonzero(new != sexp).tolist():
             uspaces[k].expected_packet_number = int(new[k])
-        return [launch[k] for k in deferred]
+        if cix:
+            ckeys = [None] * len(cix)
+            for c in conns:
+                if c is not None:
+                    ckeys[cix[id(c)]] = c
+            self._closed.update(id(ckeys[k]) for k, f in enumerate(closed) if f)
+        return list(deferred)
 
     def _launch(self, idx: list, triples: list, expected: list):
         """One unprotect launch over items idx with per-item (aead, hp,
@@ -389,9 +427,10 @@ class ReceiveBatch:
         """One round's in-order walk over the launch results, with every state
         change deferred: returns (outcomes by item, stale items, speculated
         items [(item, expected number)], pairs to roll, {space: (space, new
-        expected number)}).  Keys change only at a roll, which blocks its pair
-        for the rest of the round, so every unblocked pair still has its
-        launch-time keys.
+        expected number)}, connections closed).  Keys change only at a roll,
+        which blocks its pair for the rest of the round, so every unblocked
+        pair still has its launch-time keys.  A stale item blocks its
+        connection as well: whether it closes the connection is not known.
 
         A packet decoded under an expected number an earlier packet has since
         raised needs another launch only if its number (hence nonce) decodes
@@ -401,14 +440,23 @@ class ReceiveBatch:
         or forged packet does, whatever its number) and listed for one
         confirming launch instead of blocking its pair."""
         pairs, spaces, track, offs = self._pairs, self._spaces, self._track, self._offs
+        conns, rsv, closed = self._conns, self._rsv, self._closed
         got: dict = {}
         stale, spec, rolls = [], [], []
         blocked: set = set()
+        bconn: set = set()
+        closing: set = set()
         exp: dict = {}
         for i in todo:
             pair = pairs[i]
-            if blocked and id(pair) in blocked:
+            cid = None if conns[i] is None else id(conns[i])
+            if (blocked and id(pair) in blocked) or (bconn and cid in bconn):
                 stale.append(i)
+                if cid is not None:
+                    bconn.add(cid)
+                continue
+            if cid is not None and (cid in closed or cid in closing):
+                got[i] = ConnectionClosedError("Connection is closed")  # connection.py:756-757
                 continue
             if pair.recv.aead is None:
                 got[i] = KeyUnavailableError("Decryption key is not available")
@@ -430,18 +478,27 @@ class ReceiveBatch:
                         continue
                     blocked.add(id(pair))
                     stale.append(i)
+                    if cid is not None:
+                        bconn.add(cid)
                     continue
             if status != L.S_OK:
                 got[i] = _raise_status(status)
                 continue
             out = r_out[i]
-            got[i] = (out[0], out[1], pn)
             if i in rolled_at:
+                # the key update inside decrypt_packet stands (crypto.py:184-192)
                 rolls.append(pair)
                 blocked.add(id(pair))
+            if rsv[i] and out[0] and out[0][0] & rsv[i]:
+                # connection.py:949-960: close before :984-985 raises the number
+                got[i] = ReservedBitsError("Reserved bits must be zero")
+                if cid is not None:
+                    closing.add(cid)
+                continue
+            got[i] = (out[0], out[1], pn)
             if track[i] and pn > exp_now:
                 exp[id(space)] = (space, pn + 1)
-        return got, stale, spec, rolls, exp
+        return got, stale, spec, rolls, exp, closing
 
     def run(self) -> list:
         pairs, spaces, offs = self._pairs, self._spaces, self._offs
@@ -492,7 +549,8 @@ class ReceiveBatch:
                     rolled_at.add(i)
                     used[i] = triples[k]
             # walk in order, applying each packet's effect on its pair
-            got, stale, spec, rolls, exp = self._walk(todo, True, r_out, r_st, r_pn, r_hl, exp_at, rolled_at)
+            got, stale, spec, rolls, exp, closing = self._walk(todo, True, r_out, r_st, r_pn, r_hl, exp_at,
+                                                               rolled_at)
             if spec:
                 # failed packets whose number now decodes differently were
                 # assumed to fail again: check them all in one launch, each
@@ -502,8 +560,8 @@ class ReceiveBatch:
                 if any(x == L.S_OK for x in st):
                     # a packet the walk took for a failure authenticates now:
                     # walk the round again without assuming (rare)
-                    got, stale, spec, rolls, exp = self._walk(todo, False, r_out, r_st, r_pn, r_hl, exp_at,
-                                                              rolled_at)
+                    got, stale, spec, rolls, exp, closing = self._walk(todo, False, r_out, r_st, r_pn, r_hl,
+                                                                       exp_at, rolled_at)
                 else:
                     for i, x in zip(idx, st):
                         got[i] = _raise_status(x)
@@ -514,8 +572,10 @@ class ReceiveBatch:
                 space.expected_packet_number = v
             for pair in rolls:
                 pair._update_key("remote_update")
+            self._closed |= closing
             for i in stale:
                 r_st[i] = None
             todo = stale
         self._pairs, self._packets, self._offs, self._spaces, self._track = [], [], [], [], []
+        self._conns, self._rsv, self._closed = [], [], set()
         return outcome

@@ -1182,6 +1182,15 @@ done:
     return ret;
 }
 
+/* Host-side outcomes of the receive walks (never produced by a kernel):
+ * a packet that authenticated with a reserved bit set (connection.py:949-960),
+ * a packet of a connection the walk has closed (:756-757). */
+#define WALK_S_RESERVED 0x101
+#define WALK_S_CLOSED 0x102
+#define WALK_NO_CONN 0xffffffffu
+/* receive_short's slot_of: closed on entry / no receive key (no launch) */
+#define RS_CLOSED 0xfffffffeu
+
 /* decode_packet_number (quic/packet.py:118-132) of the truncated number as
  * HeaderProtection.remove hands it over: a signed C int (_crypto.c:349), so a
  * 4-byte value >= 2^31 enters negative, exactly as the Python walk sees it.
@@ -1201,8 +1210,10 @@ static int64_t decode_pn_signed(uint64_t pn, int pn_len, uint64_t expected)
 }
 
 /* unprotect_walk(table, slots_u32, exp_u64, packets, offs_u32, pair_u32,
- *                space_u32, track_u8, space_exp_u64, n_pairs)
- *     -> (outcomes, results, deferred, space_exp_u64 after the walk)
+ *                space_u32, track_u8, space_exp_u64, n_pairs, conn_u32,
+ *                rsv_u8, closed_u8)
+ *     -> (outcomes, results, deferred, space_exp_u64 after the walk,
+ *         closed_u8 after the walk)
  * One ReceiveBatch round in C: the launch (as unprotect_list, each packet
  * decoded against exp[i], its space's expected number when the round began)
  * and the in-order walk of CryptoPair.decrypt_packet semantics
@@ -1217,38 +1228,49 @@ static int64_t decode_pn_signed(uint64_t pn, int pn_len, uint64_t expected)
  * truncated number decodes differently under the space's expected number by
  * now than under exp[i].  The caller's general walk (batch_io.ReceiveBatch)
  * then continues with the deferred packets, in order, from the state left
- * here. */
+ * here.
+ * Connections (conn_u32[i]: the packet's connection, WALK_NO_CONN for none;
+ * rsv_u8[i]: its reserved-bit mask, 0 for no check; closed_u8: each
+ * connection's closed flag, returned updated): a packet that authenticates
+ * with a reserved bit set closes its connection (connection.py:949-960) --
+ * status WALK_S_RESERVED, no expected-number update -- and every later packet
+ * of a closed connection gets WALK_S_CLOSED (:756-757).  A deferred packet
+ * blocks its connection too: whether it closes it is not known yet. */
 static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
 {
     PyObject *t, *packets;
-    const char *a_sl, *a_exp, *a_offs, *a_pair, *a_space, *a_track, *a_sexp;
-    Py_ssize_t l_sl, l_exp, l_offs, l_pair, l_space, l_track, l_sexp;
+    const char *a_sl, *a_exp, *a_offs, *a_pair, *a_space, *a_track, *a_sexp, *a_conn, *a_rsv, *a_closed;
+    Py_ssize_t l_sl, l_exp, l_offs, l_pair, l_space, l_track, l_sexp, l_conn, l_rsv, l_closed;
     unsigned int n_pairs;
-    if (!PyArg_ParseTuple(args, "Oy#y#O!y#y#y#y#y#I", &t, &a_sl, &l_sl, &a_exp, &l_exp, &PyList_Type, &packets,
+    if (!PyArg_ParseTuple(args, "Oy#y#O!y#y#y#y#y#Iy#y#y#", &t, &a_sl, &l_sl, &a_exp, &l_exp, &PyList_Type, &packets,
                           &a_offs, &l_offs, &a_pair, &l_pair, &a_space, &l_space, &a_track, &l_track, &a_sexp,
-                          &l_sexp, &n_pairs))
+                          &l_sexp, &n_pairs, &a_conn, &l_conn, &a_rsv, &l_rsv, &a_closed, &l_closed))
         return NULL;
     qpp_keytab *kt = as_table(t);
     if (!kt) return NULL;
     const Py_ssize_t n = PyList_Size(packets);
     if (check_len(l_sl, n, 4, "slots") < 0 || check_len(l_exp, n, 8, "exp") < 0 ||
         check_len(l_offs, n, 4, "offs") < 0 || check_len(l_pair, n, 4, "pair") < 0 ||
-        check_len(l_space, n, 4, "space") < 0 || check_len(l_track, n, 1, "track") < 0 || l_sexp % 8)
+        check_len(l_space, n, 4, "space") < 0 || check_len(l_track, n, 1, "track") < 0 ||
+        check_len(l_conn, n, 4, "conn") < 0 || check_len(l_rsv, n, 1, "rsv") < 0 || l_sexp % 8)
         return l_sexp % 8 ? (PyErr_SetString(PyExc_ValueError, "space_exp: whole u64 items"), NULL) : NULL;
-    const Py_ssize_t n_spaces = l_sexp / 8;
+    const Py_ssize_t n_spaces = l_sexp / 8, n_conns = l_closed;
     const uint32_t *slots = (const uint32_t *)a_sl, *offs = (const uint32_t *)a_offs, *pair = (const uint32_t *)a_pair,
-                   *space = (const uint32_t *)a_space;
+                   *space = (const uint32_t *)a_space, *conn = (const uint32_t *)a_conn;
     const uint64_t *exp = (const uint64_t *)a_exp;
-    const uint8_t *track = (const uint8_t *)a_track;
-    PyObject *ret = NULL, *outs = NULL, *res = NULL, *deferred = NULL, *sexp_out = NULL;
+    const uint8_t *track = (const uint8_t *)a_track, *rsv = (const uint8_t *)a_rsv;
+    PyObject *ret = NULL, *outs = NULL, *res = NULL, *deferred = NULL, *sexp_out = NULL, *closed_out = NULL;
     qpp_desc *desc = NULL;
-    uint8_t *blocked_pair = NULL, *blocked_space = NULL;
+    uint8_t *blocked_pair = NULL, *blocked_space = NULL, *blocked_conn = NULL;
     sexp_out = PyBytes_FromStringAndSize(a_sexp, l_sexp);  /* the spaces' expected numbers, advanced below */
-    if (!sexp_out) return NULL;
+    closed_out = PyBytes_FromStringAndSize(a_closed, l_closed); /* the connections' closed flags, set below */
+    if (!sexp_out || !closed_out) goto done;
     uint64_t *sx = (uint64_t *)PyBytes_AsString(sexp_out);
+    uint8_t *closed = (uint8_t *)PyBytes_AsString(closed_out);
     for (Py_ssize_t i = 0; i < n; ++i)
-        if (pair[i] >= n_pairs || (Py_ssize_t)space[i] >= n_spaces) {
-            PyErr_SetString(PyExc_ValueError, "pair or space index out of range");
+        if (pair[i] >= n_pairs || (Py_ssize_t)space[i] >= n_spaces ||
+            (conn[i] != WALK_NO_CONN && (Py_ssize_t)conn[i] >= n_conns)) {
+            PyErr_SetString(PyExc_ValueError, "pair, space or connection index out of range");
             goto done;
         }
     /* sizes, then the launch over the session's pinned staging */
@@ -1265,9 +1287,10 @@ static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
     res = PyBytes_FromStringAndSize(NULL, n * (Py_ssize_t)sizeof(qpp_result));
     blocked_pair = (uint8_t *)calloc(n_pairs ? n_pairs : 1, 1);
     blocked_space = (uint8_t *)calloc(n_spaces ? (size_t)n_spaces : 1, 1);
+    blocked_conn = (uint8_t *)calloc(n_conns ? (size_t)n_conns : 1, 1);
     outs = PyList_New(n);
     deferred = PyList_New(0);
-    if (!desc || !res || !blocked_pair || !blocked_space || !outs || !deferred) {
+    if (!desc || !res || !blocked_pair || !blocked_space || !blocked_conn || !outs || !deferred) {
         PyErr_NoMemory();
         goto done;
     }
@@ -1291,13 +1314,23 @@ static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
         if (host_call(0, kt, desc, (uint32_t)n, hin, total, hout, total, PyBytes_AsString(res)) < 0) goto done;
     }
     {
-        const qpp_result *r = (const qpp_result *)PyBytes_AsString(res);
+        qpp_result *r = (qpp_result *)PyBytes_AsString(res);
+        /* no receive key (crypto.py:78-79) and packet-number offsets past the
+           header limit fail whatever the launch left in their results */
         for (Py_ssize_t i = 0; i < n; ++i) {
-            const uint32_t p = pair[i], sp = space[i];
+            if (slots[i] == 0xffffffffu) r[i].status = QPP_S_NO_KEY;
+            else if (offs[i] > QPP_MAX_HDR) r[i].status = QPP_S_LENGTH;
+        }
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            const uint32_t p = pair[i], sp = space[i], c = conn[i];
             PyObject *item = Py_None;
             Py_INCREF(Py_None);
             PyList_SetItem(outs, i, item);
-            int defer = blocked_pair[p] || blocked_space[sp];
+            int defer = blocked_pair[p] || blocked_space[sp] || (c != WALK_NO_CONN && blocked_conn[c]);
+            if (!defer && c != WALK_NO_CONN && closed[c]) {
+                r[i].status = WALK_S_CLOSED; /* connection.py:756-757 */
+                continue;
+            }
             const uint16_t st = r[i].status;
             const uint64_t now = sx[sp];
             if (!defer && st == QPP_S_KEY_PHASE) defer = 1;
@@ -1307,6 +1340,7 @@ static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
             }
             if (defer) {
                 blocked_pair[p] = blocked_space[sp] = 1;
+                if (c != WALK_NO_CONN) blocked_conn[c] = 1;
                 PyObject *ix = PyLong_FromSsize_t(i);
                 if (!ix || PyList_Append(deferred, ix) < 0) {
                     Py_XDECREF(ix);
@@ -1317,6 +1351,12 @@ static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
             }
             if (st != QPP_S_OK) continue;
             const uint8_t *o = hout + desc[i].out_off;
+            if (rsv[i] && r[i].hdr_len && (o[0] & rsv[i])) {
+                /* connection.py:949-960: close, end, no expected-number update */
+                r[i].status = WALK_S_RESERVED;
+                if (c != WALK_NO_CONN) closed[c] = 1;
+                continue;
+            }
             PyObject *h = PyBytes_FromStringAndSize((const char *)o, r[i].hdr_len);
             PyObject *pl = PyBytes_FromStringAndSize((const char *)o + r[i].hdr_len,
                                                      (Py_ssize_t)r[i].out_len - r[i].hdr_len);
@@ -1331,15 +1371,17 @@ static PyObject *py_unprotect_walk(PyObject *m, PyObject *args)
             if (track[i] && r[i].pn > now) sx[sp] = r[i].pn + 1;
         }
     }
-    ret = PyTuple_Pack(4, outs, res, deferred, sexp_out);
+    ret = PyTuple_Pack(5, outs, res, deferred, sexp_out, closed_out);
 done:
     Py_XDECREF(sexp_out);
+    Py_XDECREF(closed_out);
     Py_XDECREF(outs);
     Py_XDECREF(res);
     Py_XDECREF(deferred);
     free(desc);
     free(blocked_pair);
     free(blocked_space);
+    free(blocked_conn);
     return ret;
 }
 
@@ -1447,8 +1489,8 @@ static PyObject *make_record(PyTypeObject *tp, allocfunc alloc, PyObject *const 
 
 /* receive_short(table, items, conns, conn_cid_u32, conn_pair_u32,
  *               conn_space_u32, pair_slot_u32, space_exp_u64, rec_type,
- *               packet_type, epoch)
- *     -> None | (records, deferred, space_exp after)
+ *               packet_type, epoch, conn_closed_u8)
+ *     -> None | (records, deferred, space_exp after, conn_closed after)
  * receive_datagrams' steady state in one call: every datagram of `items`
  * ((connection, bytes) pairs) is a short-header 1-RTT packet running to the
  * datagram's end (RFC 9000 sec. 12.2), its encrypted offset 1 + the
@@ -1458,19 +1500,24 @@ static PyObject *make_record(PyTypeObject *tp, allocfunc alloc, PyObject *const 
  * record per datagram:
  *   (datagram, 0, None, packet_type, epoch, plain_header, payload, pn, None),
  *   or the drop: "key_unavailable" (pair_slot 0xffffffff: no receive key,
- *   crypto.py:78-79) / "payload_decrypt_error" (connection.py:936-947).
+ *   crypto.py:78-79) / "payload_decrypt_error" (connection.py:936-947) /
+ *   "reserved_bits" (a packet that authenticates with a reserved bit set
+ *   closes its connection, connection.py:949-960, and leaves the expected
+ *   number alone) / "connection_closed" (epoch None: a datagram of a closed
+ *   connection, ignored by connection.py:756-757; nothing is launched for the
+ *   connections closed on entry).
  * Deferred datagrams (key-phase flip, or a number that decodes differently
- * by now -- and every later one of their pair or space) get None and their
+ * by now -- and every later one of their pair, space or connection) get None and their
  * index in `deferred`, for the caller's general path.  Returns None at once,
  * with nothing launched, if any datagram is not such a packet. */
 static PyObject *py_receive_short(PyObject *m, PyObject *args)
 {
     PyObject *t, *items, *conns, *rec_type, *ptype, *epoch;
-    const char *a_cid, *a_pair, *a_space, *a_pslot, *a_sexp;
-    Py_ssize_t l_cid, l_pair, l_space, l_pslot, l_sexp;
-    if (!PyArg_ParseTuple(args, "OO!O!y#y#y#y#y#OOO", &t, &PyList_Type, &items, &PyList_Type, &conns, &a_cid, &l_cid,
-                          &a_pair, &l_pair, &a_space, &l_space, &a_pslot, &l_pslot, &a_sexp, &l_sexp, &rec_type,
-                          &ptype, &epoch))
+    const char *a_cid, *a_pair, *a_space, *a_pslot, *a_sexp, *a_closed;
+    Py_ssize_t l_cid, l_pair, l_space, l_pslot, l_sexp, l_closed;
+    if (!PyArg_ParseTuple(args, "OO!O!y#y#y#y#y#OOOy#", &t, &PyList_Type, &items, &PyList_Type, &conns, &a_cid,
+                          &l_cid, &a_pair, &l_pair, &a_space, &l_space, &a_pslot, &l_pslot, &a_sexp, &l_sexp,
+                          &rec_type, &ptype, &epoch, &a_closed, &l_closed))
         return NULL;
     qpp_keytab *kt = as_table(t);
     if (!kt) return NULL;
@@ -1481,7 +1528,7 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     const Py_ssize_t n = PyList_Size(items), nc = PyList_Size(conns);
     const Py_ssize_t n_pairs = l_pslot / 4, n_spaces = l_sexp / 8;
     if (check_len(l_cid, nc, 4, "conn_cid") < 0 || check_len(l_pair, nc, 4, "conn_pair") < 0 ||
-        check_len(l_space, nc, 4, "conn_space") < 0)
+        check_len(l_space, nc, 4, "conn_space") < 0 || check_len(l_closed, nc, 1, "conn_closed") < 0)
         return NULL;
     const uint32_t *ccid = (const uint32_t *)a_cid, *cpair = (const uint32_t *)a_pair,
                    *cspace = (const uint32_t *)a_space, *pslot = (const uint32_t *)a_pslot;
@@ -1500,9 +1547,9 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     uint8_t **cd = NULL;
     const uint8_t **cs = NULL;
     size_t *cl = NULL;
-    uint8_t *blocked_pair = NULL, *blocked_space = NULL;
-    PyObject *ret = NULL, *recs = NULL, *res = NULL, *deferred = NULL, *sexp_out = NULL;
-    PyObject *empty = NULL, *minus1 = NULL, *zero = NULL, *s_key = NULL, *s_dec = NULL;
+    uint8_t *blocked_pair = NULL, *blocked_space = NULL, *blocked_conn = NULL;
+    PyObject *ret = NULL, *recs = NULL, *res = NULL, *deferred = NULL, *sexp_out = NULL, *closed_out = NULL;
+    PyObject *empty = NULL, *minus1 = NULL, *zero = NULL, *s_key = NULL, *s_dec = NULL, *s_rsv = NULL, *s_closed = NULL;
     uint8_t **od = NULL;
     const uint8_t **os_ = NULL;
     size_t *ol = NULL, on = 0, otot = 0;
@@ -1517,12 +1564,14 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     cl = (size_t *)malloc((n ? (size_t)n : 1) * sizeof(size_t));
     blocked_pair = (uint8_t *)calloc(n_pairs ? (size_t)n_pairs : 1, 1);
     blocked_space = (uint8_t *)calloc(n_spaces ? (size_t)n_spaces : 1, 1);
+    blocked_conn = (uint8_t *)calloc(nc ? (size_t)nc : 1, 1);
     /* output copies: header and payload of every packet, filled after the
        walk without the GIL (the bytes objects are not shared until returned) */
     od = (uint8_t **)malloc((2 * (size_t)n + 1) * sizeof(uint8_t *));
     os_ = (const uint8_t **)malloc((2 * (size_t)n + 1) * sizeof(uint8_t *));
     ol = (size_t *)malloc((2 * (size_t)n + 1) * sizeof(size_t));
-    if (!conn_of || !slot_of || !desc || !cd || !cs || !cl || !blocked_pair || !blocked_space || !od || !os_ || !ol)
+    if (!conn_of || !slot_of || !desc || !cd || !cs || !cl || !blocked_pair || !blocked_space || !blocked_conn || !od ||
+        !os_ || !ol)
         goto nomem;
     /* classify: every datagram a short header long enough for its CID */
     size_t total = 0;
@@ -1538,8 +1587,8 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
         const uint8_t *b = (const uint8_t *)PyBytes_AsString(d);
         if (len < 1 || (b[0] & 0xC0) != 0x40 || len < 1 + (Py_ssize_t)ccid[found]) goto fallback;
         conn_of[i] = (uint32_t)found;
-        slot_of[i] = pslot[cpair[found]];
-        if (slot_of[i] == 0xffffffffu) continue; /* no receive key: no launch */
+        slot_of[i] = ((const uint8_t *)a_closed)[found] ? RS_CLOSED : pslot[cpair[found]];
+        if (slot_of[i] >= RS_CLOSED) continue; /* closed on entry, or no receive key: no launch */
         qpp_desc *x = &desc[nl];
         x->in_off = x->out_off = total;
         x->len = (uint32_t)len;
@@ -1554,6 +1603,7 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     }
     res = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)nl * (Py_ssize_t)sizeof(qpp_result));
     sexp_out = PyBytes_FromStringAndSize(a_sexp, l_sexp);
+    closed_out = PyBytes_FromStringAndSize(a_closed, l_closed);
     recs = PyList_New(n);
     deferred = PyList_New(0);
     empty = PyBytes_FromStringAndSize("", 0);
@@ -1561,7 +1611,11 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     zero = PyLong_FromLong(0);
     s_key = PyUnicode_FromString("key_unavailable");
     s_dec = PyUnicode_FromString("payload_decrypt_error");
-    if (!res || !sexp_out || !recs || !deferred || !empty || !minus1 || !zero || !s_key || !s_dec) goto nomem;
+    s_rsv = PyUnicode_FromString("reserved_bits");
+    s_closed = PyUnicode_FromString("connection_closed");
+    if (!res || !sexp_out || !closed_out || !recs || !deferred || !empty || !minus1 || !zero || !s_key || !s_dec ||
+        !s_rsv || !s_closed)
+        goto nomem;
     uint8_t *hin = NULL, *hout = NULL;
     if (nl) {
         qpp_session *ss = session();
@@ -1574,37 +1628,54 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     }
     {
         uint64_t *sx = (uint64_t *)PyBytes_AsString(sexp_out);
+        uint8_t *closed = (uint8_t *)PyBytes_AsString(closed_out);
         const qpp_result *r = (const qpp_result *)PyBytes_AsString(res);
         uint32_t k = 0;
         for (Py_ssize_t i = 0; i < n; ++i) {
             PyObject *di = PyLong_FromSsize_t(i);
             if (!di) goto done;
             const uint32_t c = conn_of[i], p = cpair[c], sp = cspace[c];
-            PyObject *rec = NULL;
-            if (slot_of[i] == 0xffffffffu) {
-                PyObject *f[9] = {di, zero, Py_None, ptype, epoch, empty, empty, minus1, s_key};
-                rec = make_record(tp, alloc, f, 9);
-            } else {
-                const qpp_result *ri = &r[k];
-                const qpp_desc *dk = &desc[k];
-                ++k;
+            const int launched = slot_of[i] < RS_CLOSED;
+            const qpp_result *ri = launched ? &r[k] : NULL;
+            const qpp_desc *dk = launched ? &desc[k] : NULL;
+            k += launched;
+            /* a deferred packet of the connection may close it: wait for it */
+            int defer = blocked_conn[c];
+            if (!defer && launched) {
                 const uint64_t now = sx[sp];
-                int defer = blocked_pair[p] || blocked_space[sp] || ri->status == QPP_S_KEY_PHASE;
-                if (!defer && now != dk->pn && (ri->status == QPP_S_OK || ri->status == QPP_S_DECRYPT)) {
+                defer = blocked_pair[p] || blocked_space[sp] || (!closed[c] && ri->status == QPP_S_KEY_PHASE);
+                if (!defer && !closed[c] && now != dk->pn && (ri->status == QPP_S_OK || ri->status == QPP_S_DECRYPT)) {
                     const int pn_len = (int)ri->hdr_len - (int)dk->hdr_len;
                     if (pn_len < 1 || pn_len > 4 || decode_pn_signed(ri->pn, pn_len, now) != (int64_t)ri->pn)
                         defer = 1;
                 }
-                if (defer) {
-                    blocked_pair[p] = blocked_space[sp] = 1;
-                    const int bad = PyList_Append(deferred, di);
-                    Py_INCREF(Py_None);
-                    PyList_SetItem(recs, i, Py_None);
-                    Py_DECREF(di);
-                    if (bad < 0) goto done;
-                    continue;
-                }
-                if (ri->status == QPP_S_OK) {
+            }
+            if (defer) {
+                blocked_conn[c] = 1;
+                if (launched) blocked_pair[p] = blocked_space[sp] = 1;
+                const int bad = PyList_Append(deferred, di);
+                Py_INCREF(Py_None);
+                PyList_SetItem(recs, i, Py_None);
+                Py_DECREF(di);
+                if (bad < 0) goto done;
+                continue;
+            }
+            PyObject *rec = NULL;
+            if (closed[c]) {
+                /* connection.py:756-757 */
+                PyObject *f[9] = {di, zero, Py_None, ptype, Py_None, empty, empty, minus1, s_closed};
+                rec = make_record(tp, alloc, f, 9);
+            } else if (!launched) {
+                PyObject *f[9] = {di, zero, Py_None, ptype, epoch, empty, empty, minus1, s_key};
+                rec = make_record(tp, alloc, f, 9);
+            } else {
+                const uint64_t now = sx[sp];
+                if (ri->status == QPP_S_OK && (hout[dk->out_off] & 0x18)) {
+                    /* connection.py:949-960: the close, before :984-985 */
+                    closed[c] = 1;
+                    PyObject *f[9] = {di, zero, Py_None, ptype, epoch, empty, empty, minus1, s_rsv};
+                    rec = make_record(tp, alloc, f, 9);
+                } else if (ri->status == QPP_S_OK) {
                     const uint8_t *o = hout + dk->out_off;
                     const size_t pll = (size_t)ri->out_len - ri->hdr_len;
                     PyObject *h = PyBytes_FromStringAndSize(NULL, ri->hdr_len);
@@ -1635,7 +1706,7 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     Py_BEGIN_ALLOW_THREADS
     par_copy(od, os_, ol, on, otot);
     Py_END_ALLOW_THREADS
-    ret = PyTuple_Pack(3, recs, deferred, sexp_out);
+    ret = PyTuple_Pack(4, recs, deferred, sexp_out, closed_out);
     goto done;
 fallback:
     Py_INCREF(Py_None);
@@ -1646,7 +1717,10 @@ nomem:
 done:
     ptrmap_free(&pm);
     free(conn_of), free(slot_of), free(desc), free(cd), free(cs), free(cl), free(blocked_pair), free(blocked_space);
-    free(od), free(os_), free(ol);
+    free(blocked_conn), free(od), free(os_), free(ol);
+    Py_XDECREF(closed_out);
+    Py_XDECREF(s_rsv);
+    Py_XDECREF(s_closed);
     Py_XDECREF(zero);
     Py_XDECREF(recs);
     Py_XDECREF(res);
@@ -1696,6 +1770,17 @@ static PyObject *py_abi(PyObject *m, PyObject *unused)
     return PyLong_FromLong(qpp_abi_version());
 }
 
+#ifndef QPP_SOURCE_HASH
+#error "build with -DQPP_SOURCE_HASH (aioquic_amd/build.py)"
+#endif
+/* the marker build.py reads back from the built extension */
+static const char kSourceHash[] = "qpp-source-hash:" QPP_SOURCE_HASH;
+
+static PyObject *py_source_hash(PyObject *m, PyObject *unused)
+{
+    return PyUnicode_FromString(kSourceHash + 16);
+}
+
 static PyMethodDef module_methods[] = {
     {"protect", py_protect, METH_VARARGS, "protect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream, plan=None)"},
     {"unprotect", py_unprotect, METH_VARARGS, "unprotect(table, desc_ptr, n, in_ptr, out_ptr, res_ptr, stream, plan=None)"},
@@ -1712,7 +1797,7 @@ static PyMethodDef module_methods[] = {
      "protect_datagrams(table, plains, dg_u32, off_u32, hsize_u32, size_u32, pn_u64, slot_u32) -> (wires, results)"},
     {"unprotect_walk", py_unprotect_walk, METH_VARARGS,
      "unprotect_walk(table, slots_u32, exp_u64, packets, offs_u32, pair_u32, space_u32, track_u8, space_exp_u64, "
-     "n_pairs) -> (outcomes, results, deferred)"},
+     "n_pairs, conn_u32, rsv_u8, closed_u8) -> (outcomes, results, deferred, space_exp, closed)"},
     {"first_of_each", py_first_of_each, METH_VARARGS, "first_of_each(items) -> distinct first elements, by identity"},
     {"receive_short", py_receive_short, METH_VARARGS,
      "receive_short(table, items, conns, conn_cid_u32, conn_pair_u32, conn_space_u32, pair_slot_u32, space_exp_u64, "
@@ -1720,6 +1805,7 @@ static PyMethodDef module_methods[] = {
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},
+    {"source_hash", py_source_hash, METH_NOARGS, "hash of the native sources this module was built from"},
     {NULL},
 };
 
@@ -1737,8 +1823,37 @@ static int add_type(PyObject *m, PyType_Spec *spec, const char *name, PyObject *
     return PyModule_AddObject(m, name, t);
 }
 
+/* Refuse a stale build: libquicpp.so and this extension must come from the
+ * same sources, and those must be the tree's current ones (when present). */
+static int check_sources(void)
+{
+    const char *mine = kSourceHash + 16, *lib = qpp_source_hash();
+    if (strcmp(mine, lib) != 0) {
+        PyErr_Format(PyExc_ImportError,
+                     "aioquic_amd: libquicpp.so (sources %s) and _crypto (sources %s) come from different "
+                     "builds; run python -m aioquic_amd.build", lib, mine);
+        return -1;
+    }
+    PyObject *mod = PyImport_ImportModule("aioquic_amd._srchash");
+    if (!mod) return -1;
+    PyObject *tree = PyObject_CallMethod(mod, "tree_hash", NULL);
+    Py_DECREF(mod);
+    if (!tree) return -1;
+    int rc = 0;
+    if (tree != Py_None && PyUnicode_CompareWithASCIIString(tree, mine) != 0) {
+        if (!PyErr_Occurred())
+            PyErr_Format(PyExc_ImportError,
+                         "aioquic_amd: the native sources (%S) changed since _crypto was built (%s); "
+                         "run python -m aioquic_amd.build", tree, mine);
+        rc = -1;
+    }
+    Py_DECREF(tree);
+    return rc;
+}
+
 PyMODINIT_FUNC PyInit__crypto(void)
 {
+    if (check_sources() < 0) return NULL;
     PyObject *m = PyModule_Create(&moduledef);
     if (!m) return NULL;
     g_crypto_error = PyErr_NewException("aioquic_amd._crypto.CryptoError", PyExc_ValueError, NULL);

@@ -16,6 +16,15 @@ Datagrams whose first byte is a short header (the 1-RTT bulk) take a
 vectorised path: encrypted offset = 1 + host CID length, one packet per
 datagram (a short-header packet always runs to the end of its datagram,
 RFC 9000 sec. 12.2), no per-packet header parse.
+
+The connection-level checks around the decrypt follow the reference too:
+a connection that lists its host CIDs drops packets for other CIDs (clients:
+every packet, servers: Handshake packets, "unknown_connection_id",
+connection.py:830-848); a packet that authenticates with a reserved header bit
+set closes its connection ("reserved_bits", :949-960: the rest of the datagram
+is not read and the expected packet number is not raised), and a closed
+connection's datagrams are ignored ("connection_closed", :756-757; one record
+per datagram, where the reference logs nothing).
 """
 
 from __future__ import annotations
@@ -27,7 +36,7 @@ import numpy as np
 
 from . import _crypto
 from ._crypto import CryptoError
-from .batch_io import ReceiveBatch, default_slots
+from .batch_io import ConnectionClosedError, ReceiveBatch, ReservedBitsError, default_slots
 from .buffer import Buffer
 from .crypto import KeyUnavailableError
 from .packet import (
@@ -55,7 +64,10 @@ class ConnectionKeys:
     """What receive_datagram consults per packet: the crypto pairs per epoch
     (Initial ones per version), the packet number spaces, the CID length,
     the role and the versions the configuration accepts
-    (QuicConfiguration.supported_versions, configuration.py:115-120)."""
+    (QuicConfiguration.supported_versions, configuration.py:115-120); the
+    host CIDs a packet's destination CID must match (connection.py:830-848;
+    None: not checked, the batch is already demultiplexed per connection) and
+    whether the connection is closing (set by a reserved-bit violation)."""
 
     cryptos: Dict[Epoch, Any]
     spaces: Dict[Epoch, Any]
@@ -64,6 +76,14 @@ class ConnectionKeys:
     is_client: bool = False
     supported_versions: List[int] = field(
         default_factory=lambda: [QuicProtocolVersion.VERSION_1, QuicProtocolVersion.VERSION_2])
+    host_cids: Optional[Sequence[bytes]] = None
+    closed: bool = False
+
+    def cid_unknown(self, packet_type: QuicPacketType, dcid: bytes) -> bool:
+        """connection.py:830-848: clients check every packet, servers their
+        Handshake packets."""
+        return (self.host_cids is not None and (self.is_client or packet_type == QuicPacketType.HANDSHAKE)
+                and dcid not in self.host_cids)
 
     def pair_and_space(self, epoch: Epoch, version: Optional[int]):
         if epoch == Epoch.INITIAL:
@@ -94,6 +114,24 @@ class ReceivedPacket(NamedTuple):
 
 
 _new = tuple.__new__
+# reserved header bits (connection.py:949-953)
+_RSV_SHORT, _RSV_LONG = 0x18, 0x0C
+_DROP_OF = {ReservedBitsError: "reserved_bits", ConnectionClosedError: "connection_closed",
+            KeyUnavailableError: "key_unavailable"}
+
+
+def _record(f: tuple, res) -> ReceivedPacket:
+    """The record of a queued packet from its ReceiveBatch outcome."""
+    if isinstance(res, tuple):
+        return _new(ReceivedPacket, f + res + (None,))
+    drop = _DROP_OF.get(type(res), "payload_decrypt_error")
+    if drop == "connection_closed":
+        f = (f[0], 0, None, QuicPacketType.ONE_RTT, None)
+    return _new(ReceivedPacket, f + (b"", b"", -1, drop))
+
+
+def _closed_record(d: int) -> ReceivedPacket:
+    return ReceivedPacket(d, 0, None, QuicPacketType.ONE_RTT, None, dropped="connection_closed")
 
 
 def _walk_long(conn: ConnectionKeys, d: int, data: bytes, out: list, queued: list, add) -> None:
@@ -114,6 +152,9 @@ def _walk_long(conn: ConnectionKeys, d: int, data: bytes, out: list, queued: lis
             out.append(ReceivedPacket(d, start, header, ptype, Epoch.INITIAL,
                                       dropped="initial_packet_datagram_too_small"))
             return
+        if conn.cid_unknown(ptype, header.destination_cid):
+            out.append(ReceivedPacket(d, start, header, ptype, None, dropped="unknown_connection_id"))
+            return
         if ptype == QuicPacketType.VERSION_NEGOTIATION:
             # not packet-protected: handed back for the connection's own handler
             out.append(ReceivedPacket(d, start, header, ptype, None))
@@ -133,7 +174,7 @@ def _walk_long(conn: ConnectionKeys, d: int, data: bytes, out: list, queued: lis
         buf.seek(end)
         queued.append((len(out), (d, start, header, ptype, epoch)))
         out.append(None)
-        add(pair, data[start:end], enc_off, space)
+        add(pair, data[start:end], enc_off, space, conn, _RSV_SHORT if ptype == QuicPacketType.ONE_RTT else _RSV_LONG)
 
 
 def _receive_short(items: list) -> Optional[List[ReceivedPacket]]:
@@ -141,6 +182,8 @@ def _receive_short(items: list) -> Optional[List[ReceivedPacket]]:
     short-header packet.  None (nothing launched) when any is not; the
     caller then walks the batch in Python."""
     conns = _crypto.first_of_each(items)
+    if any(c.is_client and c.host_cids is not None for c in conns):
+        return None  # DCID checks: the general walk
     pix: dict = {}
     six: dict = {}
     upairs, uspaces, c_pair, c_space, c_cid = [], [], [], [], []
@@ -165,13 +208,16 @@ def _receive_short(items: list) -> Optional[List[ReceivedPacket]]:
     got = _crypto.receive_short(slots.table, items, conns, np.asarray(c_cid, np.uint32).tobytes(),
                                 np.asarray(c_pair, np.uint32).tobytes(), np.asarray(c_space, np.uint32).tobytes(),
                                 pslot.tobytes(), sexp.tobytes(), ReceivedPacket, QuicPacketType.ONE_RTT,
-                                Epoch.ONE_RTT)
+                                Epoch.ONE_RTT, bytes(bool(c.closed) for c in conns))
     if got is None:
         return None
-    recs, deferred, sexp2 = got
+    recs, deferred, sexp2, closed = got
     new = np.frombuffer(sexp2, dtype=np.uint64)
     for k in np.flatnonzero(new != sexp).tolist():
         uspaces[k].expected_packet_number = int(new[k])
+    for k, f in enumerate(closed):
+        if f:
+            conns[k].closed = True
     if deferred:
         # key-phase flips and numbers decoded under a stale expected number:
         # the general walk takes them in order from the state left above
@@ -179,15 +225,11 @@ def _receive_short(items: list) -> Optional[List[ReceivedPacket]]:
         for d in deferred:
             conn, data = items[d]
             pair, space = conn.pair_and_space(Epoch.ONE_RTT, None)
-            rb.add(pair, data, 1 + conn.host_cid_length, space=space)
+            rb.add(pair, data, 1 + conn.host_cid_length, space=space, conn=conn, reserved_mask=_RSV_SHORT)
         for d, res in zip(deferred, rb.run()):
-            f = (d, 0, None, QuicPacketType.ONE_RTT, Epoch.ONE_RTT)
-            if isinstance(res, tuple):
-                recs[d] = _new(ReceivedPacket, f + res + (None,))
-            elif isinstance(res, KeyUnavailableError):
-                recs[d] = _new(ReceivedPacket, f + (b"", b"", -1, "key_unavailable"))
-            else:
-                recs[d] = _new(ReceivedPacket, f + (b"", b"", -1, "payload_decrypt_error"))
+            recs[d] = _record((d, 0, None, QuicPacketType.ONE_RTT, Epoch.ONE_RTT), res)
+            if isinstance(res, ReservedBitsError):
+                items[d][0].closed = True
     return recs
 
 
@@ -218,45 +260,77 @@ def receive_datagrams(items: Sequence[Tuple[ConnectionKeys, bytes]],
     r_packets: list = []
     r_offs: list = []
     r_spaces: list = []
+    r_conns: list = []
     by_conn: dict = {}
     bulk = own or hasattr(batch, "_extend")
 
     def flush_run():
         if r_pairs:
             if bulk:
-                batch._extend(r_pairs, r_packets, r_offs, r_spaces)
+                batch._extend(r_pairs, r_packets, r_offs, r_spaces, r_conns, _RSV_SHORT)
             else:
-                for a, b, c, e in zip(r_pairs, r_packets, r_offs, r_spaces):
-                    batch.add(a, b, c, space=e)
-            r_pairs.clear(), r_packets.clear(), r_offs.clear(), r_spaces.clear()
+                for a, b, c, e, g in zip(r_pairs, r_packets, r_offs, r_spaces, r_conns):
+                    batch.add(a, b, c, space=e, conn=g, reserved_mask=_RSV_SHORT)
+            r_pairs.clear(), r_packets.clear(), r_offs.clear(), r_spaces.clear(), r_conns.clear()
 
-    def add(pair, packet, enc_off, space):
+    def add(pair, packet, enc_off, space, conn, rsv):
         flush_run()
-        batch.add(pair, packet, enc_off, space=space)
+        batch.add(pair, packet, enc_off, space=space, conn=conn, reserved_mask=rsv)
 
     one_rtt, ep1 = QuicPacketType.ONE_RTT, Epoch.ONE_RTT
     for d, ((conn, data), is_short) in enumerate(zip(items, short)):
+        if conn.closed:
+            out.append(_closed_record(d))  # connection.py:756-757
+            continue
         if is_short:
             c = by_conn.get(id(conn))
             if c is None:
                 pair, space = conn.pair_and_space(ep1, None)
-                c = by_conn[id(conn)] = (pair, space, 1 + conn.host_cid_length, conn)
+                c = by_conn[id(conn)] = (pair, space, 1 + conn.host_cid_length, conn,
+                                         conn.is_client and conn.host_cids is not None)
             if len(data) >= c[2]:
+                if c[4] and data[1:c[2]] not in conn.host_cids:
+                    out.append(ReceivedPacket(d, 0, None, one_rtt, None, dropped="unknown_connection_id"))
+                    continue
                 queued.append((len(out), (d, 0, None, one_rtt, ep1)))
                 out.append(None)
                 r_pairs.append(c[0])
                 r_packets.append(data)
                 r_offs.append(c[2])
                 r_spaces.append(c[1])
+                r_conns.append(conn)
                 continue
         _walk_long(conn, d, data, out, queued, add)
     flush_run()
     results = batch.run()
+    cut = False
     for (pos, f), res in zip(queued, results):
-        if isinstance(res, tuple):
-            out[pos] = _new(ReceivedPacket, f + res + (None,))
-        elif isinstance(res, KeyUnavailableError):
-            out[pos] = _new(ReceivedPacket, f + (b"", b"", -1, "key_unavailable"))
+        out[pos] = _record(f, res)
+        cut = cut or not isinstance(res, tuple) and isinstance(res, (ReservedBitsError, ConnectionClosedError))
+    return _apply_closes(items, out) if cut else out
+
+
+def _apply_closes(items, out: list) -> list:
+    """A reserved-bit violation closes its connection (connection.py:949-960):
+    the rest of its datagram is not read, and every later datagram of the
+    connection is ignored (:756-757), one "connection_closed" record each."""
+    new: list = []
+    closed: set = set()
+    k = 0
+    while k < len(out):
+        d = out[k].datagram
+        conn = items[d][0]
+        e = k
+        while e < len(out) and out[e].datagram == d:
+            e += 1
+        if id(conn) in closed:
+            new.append(_closed_record(d))
         else:
-            out[pos] = _new(ReceivedPacket, f + (b"", b"", -1, "payload_decrypt_error"))
-    return out
+            for r in out[k:e]:
+                new.append(r)
+                if r.dropped == "reserved_bits":
+                    closed.add(id(conn))
+                    conn.closed = True
+                    break
+        k = e
+    return new

@@ -132,6 +132,9 @@ typedef struct qpp_session qpp_session; /* pinned staging + device buffers + str
 
 /* library / device */
 int qpp_abi_version(void);
+/* 16 hex digits: the hash of the native sources the library was built from
+ * (aioquic_amd/_srchash.py); a binding checks it against its own at load. */
+const char *qpp_source_hash(void);
 const char *qpp_strerror(int rc);
 int qpp_device_check(void);             /* QPP_OK if the current device is gfx950 */
 

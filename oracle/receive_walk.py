@@ -5,17 +5,22 @@ TEST INFRASTRUCTURE ONLY: imported by tests/, never by the product package.
 
 It restates, one packet at a time and independently of aioquic_amd:
   * pull_quic_header           src/aioquic/quic/packet.py:181-267
-  * QuicConnection.receive_datagram's loop, up to the decrypt and the
-    expected-packet-number update   src/aioquic/quic/connection.py:793-947,984-985
+  * QuicConnection.receive_datagram's loop, up to the decrypt, the
+    reserved-bits check and the expected-packet-number update
+    src/aioquic/quic/connection.py:756-757,793-960,984-985
     (drop triggers: header_parse_error :800-810, initial_packet_datagram_too_small
-    :814-828, unsupported_version :856-869, key_unavailable :914-935,
-    payload_decrypt_error :936-947; Version Negotiation :851-853 and Retry
-    :872-880 are handed back unprotected)
+    :814-828, unknown_connection_id :830-848, unsupported_version :856-869,
+    key_unavailable :914-935, payload_decrypt_error :936-947; Version
+    Negotiation :851-853 and Retry :872-880 are handed back unprotected;
+    "reserved_bits" is the close of :949-960, which ends the datagram and
+    leaves the expected packet number alone; "connection_closed" stands for a
+    datagram that :756-757 ignores because the connection is closing)
   * CryptoPair / CryptoContext.decrypt_packet with the key-phase roll
     src/aioquic/quic/crypto.py:75-103,148-168,184-192,243-246
 with the packet arithmetic from the C oracle (oracle.unprotect / hp_mask).
-The connection-ID match (:830-848) is not modelled: the batched caller gets
-datagrams already demultiplexed per connection (asyncio/server.py:60-152).
+The connection-ID match (:830-848) runs when the connection lists its host
+CIDs; without them the batched caller's datagrams are taken as already
+demultiplexed per connection (asyncio/server.py:60-152).
 """
 
 from __future__ import annotations
@@ -69,6 +74,7 @@ class Header:
     packet_type: str
     packet_length: int
     encrypted_offset: int  # bytes from the packet start to the packet number
+    destination_cid: bytes = b""
 
 
 def parse_header(data: bytes, start: int, host_cid_length: int) -> Header:
@@ -78,16 +84,17 @@ def parse_header(data: bytes, start: int, host_cid_length: int) -> Header:
     if not first & LONG:
         if not first & FIXED:
             raise ParseError("Packet fixed bit is zero")
-        c.take(host_cid_length)
-        return Header(None, "ONE_RTT", len(data) - start, c.pos - start)
+        dcid = c.take(host_cid_length)
+        return Header(None, "ONE_RTT", len(data) - start, c.pos - start, dcid)
     version = c.u32()
+    cids = []
     for what in ("Destination", "Source"):
         n = c.u8()
         if n > 20:
             raise ParseError(f"{what} CID is too long ({n} bytes)")
-        c.take(n)
+        cids.append(c.take(n))
     if version == VERSION_NEGOTIATION:
-        return Header(version, "VERSION_NEGOTIATION", len(data) - start, c.pos - start)
+        return Header(version, "VERSION_NEGOTIATION", len(data) - start, c.pos - start, cids[0])
     if not first & FIXED:
         raise ParseError("Packet fixed bit is zero")
     ptype = (_TYPES_V2 if version == O.VERSION_2 else _TYPES_V1)[(first >> 4) & 3]
@@ -102,7 +109,7 @@ def parse_header(data: bytes, start: int, host_cid_length: int) -> Header:
     end = c.pos + rest
     if end > len(data):
         raise ParseError("Packet payload is truncated")
-    return Header(version, ptype, end - start, c.pos - start)
+    return Header(version, ptype, end - start, c.pos - start, cids[0])
 
 
 class KeyUnavailable(Exception):
@@ -166,7 +173,8 @@ class Pair:
 @dataclass
 class Conn:
     """What receive_datagram consults: pairs per epoch (Initial per version),
-    expected packet numbers per space, CID length, role, versions."""
+    expected packet numbers per space, CID length, role, versions; the host
+    CIDs (None: not checked) and whether the connection is closing."""
 
     pairs: Dict[str, Pair]
     expected: Dict[str, int] = field(default_factory=lambda: {"INITIAL": 0, "HANDSHAKE": 0, "ONE_RTT": 0})
@@ -174,6 +182,8 @@ class Conn:
     host_cid_length: int = 8
     is_client: bool = False
     supported_versions: List[int] = field(default_factory=lambda: [O.VERSION_1, O.VERSION_2])
+    host_cids: Optional[List[bytes]] = None
+    closed: bool = False
 
 
 @dataclass
@@ -192,6 +202,10 @@ def receive(items) -> List[Outcome]:
     packet (or per dropped remainder of a datagram)."""
     out: List[Outcome] = []
     for d, (conn, data) in enumerate(items):
+        if conn.closed:
+            # connection.py:756-757: a closing connection ignores the datagram
+            out.append(Outcome(d, 0, "ONE_RTT", "connection_closed"))
+            continue
         pos = 0
         while pos < len(data):
             try:
@@ -201,6 +215,12 @@ def receive(items) -> List[Outcome]:
                 break
             if not conn.is_client and h.packet_type == "INITIAL" and len(data) < 1200:
                 out.append(Outcome(d, pos, h.packet_type, "initial_packet_datagram_too_small"))
+                break
+            # connection.py:830-848: clients check every packet's DCID,
+            # servers their Handshake packets'
+            if (conn.host_cids is not None and (conn.is_client or h.packet_type == "HANDSHAKE")
+                    and h.destination_cid not in conn.host_cids):
+                out.append(Outcome(d, pos, h.packet_type, "unknown_connection_id"))
                 break
             if h.packet_type == "VERSION_NEGOTIATION":
                 out.append(Outcome(d, pos, h.packet_type))
@@ -222,12 +242,20 @@ def receive(items) -> List[Outcome]:
             try:
                 o.plain_header, o.plain_payload, o.packet_number = pair.decrypt_packet(
                     data[pos:end], h.encrypted_offset, conn.expected[space])
-                if o.packet_number > conn.expected[space]:
-                    conn.expected[space] = o.packet_number + 1
             except KeyUnavailable:
                 o.dropped = "key_unavailable"
             except DecryptError:
                 o.dropped = "payload_decrypt_error"
+            if o.dropped is None:
+                # connection.py:949-960: reserved bits set close the connection
+                # (a key update inside decrypt_packet stands) and end the
+                # datagram before :984-985 raises the expected number
+                if o.plain_header[0] & (0x18 if h.packet_type == "ONE_RTT" else 0x0C):
+                    out.append(Outcome(d, pos, h.packet_type, "reserved_bits"))
+                    conn.closed = True
+                    break
+                if o.packet_number > conn.expected[space]:
+                    conn.expected[space] = o.packet_number + 1
             out.append(o)
             pos = end
     return out

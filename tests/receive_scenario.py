@@ -8,7 +8,12 @@ triggers of the reference's receive loop (quic/connection.py:793-947):
 coalesced Initial + Handshake + 1-RTT datagrams, 0-RTT, 1-4 byte packet
 numbers, reordering, a peer key update (key-phase flip, crypto.py:91-96),
 tampered packets, too-short packets, a grease version, Version Negotiation,
-garbage, a too-small Initial datagram and a connection without 1-RTT keys.
+garbage, a too-small Initial datagram and a connection without 1-RTT keys;
+and the connection-level checks around the decrypt: a Handshake packet for an
+unknown destination CID and a client's 1-RTT packet for one (:830-848),
+packets with reserved header bits set -- a 1-RTT one after the key update and
+a long-header one inside a coalesced datagram -- that close their connection
+(:949-960), and a connection closed before the batch (:756-757).
 """
 
 from __future__ import annotations
@@ -24,10 +29,11 @@ GREASE_VERSION = 0x1A2A3A4A
 
 
 def long_header(version: int, ptype: str, dcid: bytes, scid: bytes, token: bytes, pn: int,
-                pn_len: int, rest_len: int) -> bytes:
-    """Long header with a 2-byte Length field; rest_len = payload + tag."""
+                pn_len: int, rest_len: int, reserved: int = 0) -> bytes:
+    """Long header with a 2-byte Length field; rest_len = payload + tag;
+    reserved: bits of the reserved field (0x0C) to set."""
     bits = _TYPE_BITS.get(version, _TYPE_BITS[O.VERSION_1])[ptype]
-    out = bytes([0xC0 | bits << 4 | (pn_len - 1)]) + version.to_bytes(4, "big")
+    out = bytes([0xC0 | bits << 4 | (reserved & 0x0C) | (pn_len - 1)]) + version.to_bytes(4, "big")
     out += bytes([len(dcid)]) + dcid + bytes([len(scid)]) + scid
     if ptype == "INITIAL":
         out += bytes([len(token)]) + token  # token length < 64: one-byte varint
@@ -35,8 +41,8 @@ def long_header(version: int, ptype: str, dcid: bytes, scid: bytes, token: bytes
     return out + (pn & ((1 << (8 * pn_len)) - 1)).to_bytes(pn_len, "big")
 
 
-def short_header(dcid: bytes, key_phase: int, pn: int, pn_len: int) -> bytes:
-    return bytes([0x40 | key_phase << 2 | (pn_len - 1)]) + dcid + \
+def short_header(dcid: bytes, key_phase: int, pn: int, pn_len: int, reserved: int = 0) -> bytes:
+    return bytes([0x40 | (reserved & 0x18) | key_phase << 2 | (pn_len - 1)]) + dcid + \
         (pn & ((1 << (8 * pn_len)) - 1)).to_bytes(pn_len, "big")
 
 
@@ -47,8 +53,10 @@ def _protect(ctx: W.Ctx, header: bytes, payload: bytes, pn: int) -> bytes:
 class ConnSpec:
     """Secrets of one connection as the server sees it (client -> server)."""
 
-    def __init__(self, rng, idx: int, version: int, suite: int, has_one_rtt: bool = True):
+    def __init__(self, rng, idx: int, version: int, suite: int, has_one_rtt: bool = True,
+                 check_cids: bool = False, is_client: bool = False, closed: bool = False):
         self.idx, self.version, self.suite = idx, version, suite
+        self.check_cids, self.is_client, self.closed = check_cids, is_client, closed
         self.cid = bytes([idx & 0xFF]) * 4 + rng.bytes(4)
         self.scid = rng.bytes(8)
         self.initial_secret = O.initial_secrets(self.cid, version)[0]  # client's
@@ -66,7 +74,8 @@ class ConnSpec:
                    "ZERO_RTT": W.Pair(W.Ctx(self.suite, self.zrtt_secret, self.version)),
                    "ONE_RTT": W.Pair(W.Ctx(self.suite, self.one_secret, self.version)
                                      if self.has_one_rtt else None)},
-            initial_pairs={self.version: init})
+            initial_pairs={self.version: init}, is_client=self.is_client,
+            host_cids=[self.cid] if self.check_cids else None, closed=self.closed)
 
     # the receiver's state, product side (aioquic_amd.crypto.CryptoPair)
     def product_conn(self):
@@ -97,17 +106,26 @@ class ConnSpec:
                      Epoch.ZERO_RTT: pair(self.suite, self.zrtt_secret),
                      Epoch.ONE_RTT: pair(self.suite, self.one_secret if self.has_one_rtt else None)},
             spaces={e: Space() for e in (Epoch.INITIAL, Epoch.HANDSHAKE, Epoch.ONE_RTT)},
-            cryptos_initial={self.version: init}, host_cid_length=8, is_client=False)
+            cryptos_initial={self.version: init}, host_cid_length=8, is_client=self.is_client,
+            host_cids=[self.cid] if self.check_cids else None, closed=self.closed)
 
 
-def build(seed: int = 0x7EC, n_conns: int = 9, per_conn: int = 40):
-    """-> (specs, [(conn index, datagram)]) in arrival order."""
+def build(seed: int = 0x7EC, n_conns: int = 9, per_conn: int = 40, checks: bool = True, client: bool = True):
+    """-> (specs, [(conn index, datagram)]) in arrival order.  checks: the
+    connection-level triggers (connection 1 checks Handshake DCIDs and gets a
+    Handshake packet for another CID; connection 2's 1-RTT stream carries a
+    reserved bit after its key update; connection 3's first coalesced
+    datagram has a reserved bit in its Handshake packet; connection 4 is
+    closed before the batch; with `client`, connection 5 is a client that
+    checks every DCID and gets a 1-RTT packet for another CID)."""
     rng = np.random.default_rng(seed)
     specs = []
     for c in range(n_conns):
         version = (O.VERSION_1, O.VERSION_2)[c % 2]
         suite = (O.AES_128_GCM, O.AES_256_GCM, O.CHACHA20_POLY1305)[c % 3]
-        specs.append(ConnSpec(rng, c, version, suite, has_one_rtt=(c != n_conns - 1)))
+        specs.append(ConnSpec(rng, c, version, suite, has_one_rtt=(c != n_conns - 1),
+                              check_cids=checks and (c == 1 or (client and c == 5)),
+                              is_client=checks and client and c == 5, closed=checks and c == 4))
     streams = []
     for s in specs:
         dg = []
@@ -120,8 +138,9 @@ def build(seed: int = 0x7EC, n_conns: int = 9, per_conn: int = 40):
         for ptype, ctx, pn, body in (("INITIAL", init, 0, 300), ("HANDSHAKE", hs, 0, 200),
                                      ("ZERO_RTT", zr, 0, 150)):
             pl = rng.bytes(body)
+            rsv = 0x04 if checks and s.idx == 3 and ptype == "HANDSHAKE" else 0
             hdr = long_header(s.version, ptype, s.cid, s.scid, b"tok" if ptype == "INITIAL" else b"",
-                              pn, 2, len(pl) + 16)
+                              pn, 2, len(pl) + 16, reserved=rsv)
             parts.append(_protect(ctx, hdr, pl, pn))
         used = sum(map(len, parts))
         hdr = short_header(s.cid, 0, 0, 2)
@@ -137,7 +156,8 @@ def build(seed: int = 0x7EC, n_conns: int = 9, per_conn: int = 40):
             if pn == upd:
                 cur = cur.next()
             pn_len = 1 + (pn % 4)
-            hdr = short_header(s.cid, cur.key_phase, pn, pn_len)
+            rsv = 0x08 if checks and s.idx == 2 and pn == upd + 5 else 0
+            hdr = short_header(s.cid, cur.key_phase, pn, pn_len, reserved=rsv)
             sent.append(_protect(cur, hdr, rng.bytes(int(rng.integers(4, 1150))), pn))
         # reorder two neighbours and replay an old-phase packet after the update
         sent[5], sent[6] = sent[6], sent[5]
@@ -153,6 +173,15 @@ def build(seed: int = 0x7EC, n_conns: int = 9, per_conn: int = 40):
         dg.append(_protect(hs, long_header(s.version, "HANDSHAKE", s.cid, s.scid, b"", 1, 1, len(pl) + 16), pl, 1))
         pl = rng.bytes(64)
         dg.append(_protect(zr, long_header(s.version, "ZERO_RTT", s.cid, s.scid, b"", 1, 2, len(pl) + 16), pl, 1))
+        if s.check_cids:
+            # a packet for a destination CID the connection does not own
+            other = bytes(8)
+            if s.is_client:
+                dg.insert(4, _protect(one, short_header(other, 0, 90, 2), rng.bytes(300), 90))
+            else:
+                pl = rng.bytes(120)
+                dg.append(_protect(hs, long_header(s.version, "HANDSHAKE", other, s.scid, b"", 2, 1,
+                                                   len(pl) + 16), pl, 2))
         streams.append(dg)
     # connection 0 also gets the odd ones out
     s0 = specs[0]

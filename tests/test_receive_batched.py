@@ -31,7 +31,7 @@ class _OracleBatch:
     def __init__(self, oracle, keys):
         self.o, self.keys, self.items = oracle, keys, []
 
-    def add(self, pair, packet, enc_off, space=None):
+    def add(self, pair, packet, enc_off, space=None, conn=None, reserved_mask=0):
         self.items.append((pair, packet, enc_off, space))
 
     def run(self):

@@ -160,14 +160,23 @@ def test_receive_datagrams_vs_oracle_walk():
         assert _product_tuple(g) == _oracle_tuple(w)
     kinds = {w.dropped for w in want}
     assert {None, "payload_decrypt_error", "key_unavailable", "unsupported_version", "header_parse_error",
-            "initial_packet_datagram_too_small"} <= kinds
-    # state after the batch: expected packet numbers and the rolled 1-RTT keys
+            "initial_packet_datagram_too_small", "unknown_connection_id", "reserved_bits",
+            "connection_closed"} <= kinds
+    _same_state(oconns, pconns)
+
+
+def _same_state(oconns, pconns):
+    """State after the batch: expected packet numbers, the rolled 1-RTT keys,
+    the connections the batch closed."""
+    from aioquic_amd.tls import Epoch
+
     for oc, pc in zip(oconns, pconns):
         assert oc.expected["ONE_RTT"] == pc.spaces[Epoch.ONE_RTT].expected_packet_number
         assert oc.expected["HANDSHAKE"] == pc.spaces[Epoch.HANDSHAKE].expected_packet_number
         assert oc.expected["INITIAL"] == pc.spaces[Epoch.INITIAL].expected_packet_number
+        assert oc.closed == pc.closed
         if oc.pairs["ONE_RTT"].recv is not None:
-            assert oc.pairs["ONE_RTT"].recv.key_phase == pc.cryptos[Epoch.ONE_RTT].recv.key_phase == 1
+            assert oc.pairs["ONE_RTT"].recv.key_phase == pc.cryptos[Epoch.ONE_RTT].recv.key_phase
 
 
 @pytest.mark.gpu
@@ -290,7 +299,7 @@ def test_receive_datagrams_short_only_vs_oracle_walk(monkeypatch):
     from aioquic_amd import receive as R
     from aioquic_amd.tls import Epoch
 
-    specs, items = RS.build(seed=0x5A, n_conns=7, per_conn=90)
+    specs, items = RS.build(seed=0x5A, n_conns=7, per_conn=90, client=False)
     items = [(c, d) for c, d in items if d and (d[0] & 0xC0) == 0x40 and len(d) >= 9]
     calls = []
     real = _crypto.receive_short
@@ -301,6 +310,106 @@ def test_receive_datagrams_short_only_vs_oracle_walk(monkeypatch):
     got = R.receive_datagrams([(pconns[c], d) for c, d in items])
     assert calls == [1]
     assert [_product_tuple(g) for g in got] == [_oracle_tuple(w) for w in want]
-    assert {"payload_decrypt_error", "key_unavailable", None} <= {w.dropped for w in want}
+    assert {"payload_decrypt_error", "key_unavailable", "reserved_bits", "connection_closed",
+            None} <= {w.dropped for w in want}
     for oc, pc in zip(oconns, pconns):
         assert oc.expected["ONE_RTT"] == pc.spaces[Epoch.ONE_RTT].expected_packet_number
+        assert oc.closed == pc.closed
+
+
+def test_oracle_connection_checks_cpu():
+    """The oracle walk's connection-level branches on the scenario (CPU):
+    the reserved-bit close ends its datagram without raising the expected
+    number, every later datagram of the connection is ignored, a connection
+    closed before the batch is ignored whole, and a DCID the connection does
+    not own ends the datagram (connection.py:756-757,830-848,949-960,984-985).
+    The reference's own walk tests need `cryptography`, absent here: these
+    semantics are restated from the source, parity unpinned against the
+    reference's outputs."""
+    specs, items = RS.build()
+    oconns = [s.oracle_conn() for s in specs]
+    out = W.receive([(oconns[c], d) for c, d in items])
+    by_dg = {}
+    for o in out:
+        by_dg.setdefault(o.datagram, []).append(o)
+    rsv = [o for o in out if o.dropped == "reserved_bits"]
+    assert {items[o.datagram][0] for o in rsv} == {2, 3}
+    for o in rsv:
+        c = items[o.datagram][0]
+        assert by_dg[o.datagram][-1] is o  # the rest of the datagram is not read
+        later = [d for d, (cc, _) in enumerate(items) if cc == c and d > o.datagram]
+        assert later and all([x.dropped for x in by_dg[d]] == ["connection_closed"] for d in later)
+        assert oconns[c].closed
+    # connection 3 closed in its first datagram: nothing raised its numbers
+    assert oconns[3].expected == {"INITIAL": 0, "HANDSHAKE": 0, "ONE_RTT": 0}
+    # connection 2 closed at pn upd + 5 of its 1-RTT stream: its number was not counted
+    assert oconns[2].expected["ONE_RTT"] <= 2 * 40 // 3 + 5 < oconns[0].expected["ONE_RTT"]
+    assert all(o.dropped == "connection_closed" for d, (c, _) in enumerate(items) if c == 4 for o in by_dg[d])
+    unk = [o for o in out if o.dropped == "unknown_connection_id"]
+    assert sorted((items[o.datagram][0], o.packet_type) for o in unk) == [(1, "HANDSHAKE"), (5, "ONE_RTT")]
+
+
+def test_receive_dcid_and_closed_cpu(oracle):
+    """The product's header-side connection checks need no device: a closed
+    connection's datagram and a client's packet for another CID are settled
+    before anything is queued for decryption."""
+    from aioquic_amd import receive as R
+
+    specs, items = RS.build(n_conns=6, per_conn=20)
+
+    class NoBatch:
+        def add(self, *a, **k):
+            raise AssertionError("nothing is decrypted")
+
+        _extend = add
+
+        def run(self):
+            return []
+
+    pick = [(c, d) for c, d in items if c == 4] + \
+        [(c, d) for c, d in items if c == 5 and d[0] & 0xC0 == 0x40 and d[1:9] == bytes(8)]
+    from aioquic_amd.tls import Epoch
+
+    # no keys needed: nothing reaches a decrypt (product_conn would need a device)
+    pconns = [R.ConnectionKeys(cryptos={e: None for e in Epoch}, spaces={e: None for e in Epoch},
+                               is_client=s.is_client, host_cids=[s.cid] if s.check_cids else None,
+                               closed=s.closed) for s in specs]
+    got = R.receive_datagrams([(pconns[c], d) for c, d in pick], batch=NoBatch())
+    want = W.receive([(s.oracle_conn(), d) for s, d in ((specs[c], d) for c, d in pick)])
+    assert [(p.datagram, p.offset, p.dropped) for p in got] == [(o.datagram, o.offset, o.dropped) for o in want]
+    assert {p.dropped for p in got} == {"connection_closed", "unknown_connection_id"}
+
+
+@pytest.mark.gpu
+def test_receive_batch_connection_close_vs_oracle():
+    """ReceiveBatch directly with connections and reserved-bit masks: two
+    connections' 1-RTT streams interleaved, one carrying a reserved bit after
+    its key update; outcomes, expected numbers and key phases equal the
+    oracle's packet-by-packet walk, and the closed connection's later packets
+    change nothing."""
+    from aioquic_amd.batch_io import ConnectionClosedError, ReceiveBatch, ReservedBitsError
+    from aioquic_amd.tls import Epoch
+
+    specs, items = RS.build(n_conns=4, per_conn=60)
+    sel = [(c, d) for c, d in items if c in (1, 2) and d and d[0] & 0xC0 == 0x40 and len(d) >= 29]
+    oconns = {c: specs[c].oracle_conn() for c in (1, 2)}
+    pconns = {c: specs[c].product_conn() for c in (1, 2)}
+    want = W.receive([(oconns[c], d) for c, d in sel])
+    batch = ReceiveBatch(capacity=16)
+    for c, d in sel:
+        pc = pconns[c]
+        batch.add(pc.cryptos[Epoch.ONE_RTT], d, 9, space=pc.spaces[Epoch.ONE_RTT], conn=pc, reserved_mask=0x18)
+    got = batch.run()
+    names = {ReservedBitsError: "reserved_bits", ConnectionClosedError: "connection_closed"}
+    n_closed = 0
+    for g, w in zip(got, want):
+        if isinstance(g, tuple):
+            assert w.dropped is None and g == (w.plain_header, w.plain_payload, w.packet_number)
+        else:
+            assert names.get(type(g), "payload_decrypt_error" if "decrypt" in str(g).lower() else "other") == \
+                w.dropped, (g, w.dropped)
+            n_closed += w.dropped == "connection_closed"
+    assert n_closed > 5
+    for c in (1, 2):
+        assert oconns[c].expected["ONE_RTT"] == pconns[c].spaces[Epoch.ONE_RTT].expected_packet_number
+        assert oconns[c].pairs["ONE_RTT"].recv.key_phase == pconns[c].cryptos[Epoch.ONE_RTT].recv.key_phase
