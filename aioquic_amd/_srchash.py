@@ -20,7 +20,8 @@ _EXTS = (".hip", ".h", ".c", ".cc", ".cpp")
 
 
 def source_files() -> list:
-    names = sorted(f for f in os.listdir(CSRC) if f.endswith(_EXTS))
+    # (dot files are scratch copies, e.g. tools/build_variant.py's)
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith(_EXTS) and not f.startswith("."))
     return [os.path.join(CSRC, f) for f in names] + [HEADER]
 
 

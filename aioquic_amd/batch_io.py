@@ -80,7 +80,10 @@ class KeySlots:
     between launches.
 
     Like the reference's AEAD objects, a KeySlots is not meant to be shared
-    by threads; the batched callers' default table is one per thread."""
+    by threads; the batched callers' default table is one per thread.  A
+    release that another thread triggers (a context torn down there) is
+    queued and applied by the table's own thread at its next assign(), so
+    no thread changes another's table."""
 
     def __init__(self, capacity: int = 1024) -> None:
         self.capacity = int(capacity)
@@ -90,7 +93,11 @@ class KeySlots:
         self._free: list = []
         self._by_obj: dict = {}  # id(aead or hp) -> idents using it
         self._pending: list = []
-        _holders.add(self)
+        self._owner = threading.get_ident()
+        self._inbox: list = []  # releases queued by other threads
+        self._inbox_lock = threading.Lock()
+        with _holders_lock:
+            _holders.add(self)
 
     def slot_for(self, aead, hp, key_phase: int) -> int:
         ident = (id(aead), id(hp), int(key_phase))
@@ -127,6 +134,8 @@ class KeySlots:
 
     def assign(self, triples) -> list:
         """Slots for a list of (aead, hp, key_phase), refilling the table if it overflows."""
+        if self._inbox:
+            self._drain()
         try:
             slots = [self.slot_for(*t) for t in triples]
         except OverflowError:
@@ -150,19 +159,48 @@ class KeySlots:
                 self._keep.pop(s, None)
                 self._free.append(s)
                 dropped.add(s)
+                # the ident leaves the other object's list too
+                for other in (k[0], k[1]):
+                    lst = self._by_obj.get(other)
+                    if lst is not None and other != id(o):
+                        try:
+                            lst.remove(k)
+                        except ValueError:
+                            pass
+                        if not lst:
+                            del self._by_obj[other]
         if not dropped:
             return
         self._pending = [m for m in self._pending if int(m["slot"][0]) not in dropped]
         self.table.clear(np.asarray(sorted(dropped), np.uint32).tobytes())
 
+    def _queue_release(self, objs) -> None:
+        with self._inbox_lock:
+            self._inbox.append(objs)
 
-# every live KeySlots, so that a context's teardown can release its keys
+    def _drain(self) -> None:
+        with self._inbox_lock:
+            todo, self._inbox = self._inbox, []
+        for objs in todo:
+            self.release(objs)
+
+
+# every live KeySlots, so that a context's teardown can release its keys;
+# registration and the snapshot below under one lock (a WeakSet's iterator
+# fails if another thread adds to it meanwhile)
 _holders: "weakref.WeakSet[KeySlots]" = weakref.WeakSet()
+_holders_lock = threading.Lock()
 
 
 def _release_keys(*objs) -> None:
-    for h in list(_holders):
-        h.release(objs)
+    me = threading.get_ident()
+    with _holders_lock:
+        holders = list(_holders)
+    for h in holders:
+        if h._owner == me:
+            h.release(objs)
+        else:
+            h._queue_release(objs)  # applied by the table's own thread
 
 
 crypto_mod._KEY_RELEASE_HOOKS.append(_release_keys)
@@ -202,21 +240,29 @@ def _context_of(crypto) -> CryptoContext:
 
 class _KeyRefs:
     """Distinct (aead, hp, key_phase) triples of a batch, by identity, so a
-    batch resolves key slots once per connection rather than per packet."""
+    batch resolves key slots once per connection rather than per packet
+    (with the context each came from, when given)."""
 
-    __slots__ = ("index", "triples")
+    __slots__ = ("index", "triples", "ctxs")
 
     def __init__(self) -> None:
         self.index: dict = {}
         self.triples: list = []
+        self.ctxs: list = []
 
-    def ref(self, aead, hp, key_phase: int) -> int:
+    def ref(self, aead, hp, key_phase: int, ctx=None) -> int:
         k = (id(aead), id(hp), key_phase)
         r = self.index.get(k)
         if r is None:
             r = self.index[k] = len(self.triples)
             self.triples.append((aead, hp, key_phase))
+            self.ctxs.append(ctx)
         return r
+
+    def superseded(self) -> list:
+        """AEADs whose context moved on (a key update) since they were added:
+        their release already ran, so a slot made for them now is stale."""
+        return [t[0] for t, c in zip(self.triples, self.ctxs) if c is not None and c.aead is not t[0]]
 
     def slots(self, table: KeySlots, refs: list) -> bytes:
         per = np.asarray(table.assign(self.triples), dtype=np.uint32)
@@ -251,7 +297,7 @@ class SendBatch:
             crypto._update_key("local_update")
         ctx = _context_of(crypto)
         assert ctx.is_valid(), "Encryption key is not available"
-        self._refs.append(self._keys.ref(ctx.aead, ctx.hp, ctx.key_phase))
+        self._refs.append(self._keys.ref(ctx.aead, ctx.hp, ctx.key_phase, ctx))
         self._headers.append(bytes(plain_header))
         self._payloads.append(bytes(plain_payload))
         self._pns.append(packet_number & 0xFFFFFFFFFFFFFFFF)
@@ -270,6 +316,9 @@ class SendBatch:
         slots = keys.slots(self.slots, refs)
         wires, res = protect_list(self.slots.table, slots, np.asarray(pns, np.uint64).tobytes(),
                                   headers, payloads)
+        old = keys.superseded()
+        if old:
+            self.slots.release(old)
         status = np.frombuffer(res, dtype=L.RESULT)["status"]
         bad = np.flatnonzero(status != L.S_OK)
         if len(bad):
@@ -572,6 +621,10 @@ class ReceiveBatch:
                 space.expected_packet_number = v
             for pair in rolls:
                 pair._update_key("remote_update")
+            if flip:
+                # the retry keys were this round's own: a roll builds the
+                # pair's next phase afresh
+                self.slots.release([t[0] for t in nxt_keys.values()])
             self._closed |= closing
             for i in stale:
                 r_st[i] = None

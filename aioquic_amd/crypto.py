@@ -86,7 +86,7 @@ def derive_key_iv_hp(*, cipher_suite: CipherSuite, secret: bytes, version: int) 
     return out  # type: ignore[return-value]
 
 
-def _status_error(status: int) -> CryptoError:
+def _status_error(status: int) -> Exception:
     if status == L.S_NO_KEY:
         return KeyUnavailableError("Decryption key is not available")
     if status == L.S_DECRYPT:

@@ -1084,10 +1084,15 @@ static PyObject *py_protect_datagrams(PyObject *m, PyObject *args)
         return NULL;
     qpp_keytab *kt = as_table(t);
     if (!kt) return NULL;
-    const Py_ssize_t nd = PyList_Size(plains), n = l_dg / 4;
+    const Py_ssize_t n = l_dg / 4;
     if (check_len(l_dg, n, 4, "dg") < 0 || check_len(l_off, n, 4, "off") < 0 || check_len(l_hs, n, 4, "hsize") < 0 ||
         check_len(l_sz, n, 4, "size") < 0 || check_len(l_pn, n, 8, "pn") < 0 || check_len(l_sl, n, 4, "slot") < 0)
         return NULL;
+    /* a snapshot holding a reference to every datagram: the copies below run
+       without the GIL, while another thread may change the caller's list */
+    plains = PySequence_Tuple(plains);
+    if (!plains) return NULL;
+    const Py_ssize_t nd = PyTuple_Size(plains);
     PyObject *ret = NULL, *wires = NULL, *res = NULL;
     size_t *base = NULL;
     qpp_desc *desc = NULL;
@@ -1100,7 +1105,7 @@ static PyObject *py_protect_datagrams(PyObject *m, PyObject *args)
     }
     base[0] = 0;
     for (Py_ssize_t d = 0; d < nd; ++d) {
-        PyObject *o = PyList_GetItem(plains, d);
+        PyObject *o = PyTuple_GetItem(plains, d);
         if (!PyBytes_Check(o)) {
             PyErr_SetString(PyExc_TypeError, "datagrams must be bytes");
             goto done;
@@ -1142,10 +1147,10 @@ static PyObject *py_protect_datagrams(PyObject *m, PyObject *args)
         }
         for (Py_ssize_t d = 0; d < nd; ++d) {
             cd[d] = hin + base[d];
-            cs[d] = (const uint8_t *)PyBytes_AsString(PyList_GetItem(plains, d));
+            cs[d] = (const uint8_t *)PyBytes_AsString(PyTuple_GetItem(plains, d));
             cl[d] = base[d + 1] - base[d];
         }
-        Py_BEGIN_ALLOW_THREADS  /* the list holds every datagram */
+        Py_BEGIN_ALLOW_THREADS  /* the snapshot holds every datagram */
         par_copy(cd, cs, cl, (size_t)nd, total);
         Py_END_ALLOW_THREADS
         const uint8_t *src = hin;  /* no packet: the datagrams as they are */
@@ -1177,6 +1182,7 @@ static PyObject *py_protect_datagrams(PyObject *m, PyObject *args)
 done:
     Py_XDECREF(wires);
     Py_XDECREF(res);
+    Py_DECREF(plains);
     free(base);
     free(desc);
     return ret;
@@ -1540,6 +1546,11 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     PyTypeObject *tp = (PyTypeObject *)rec_type;
     allocfunc alloc = (allocfunc)PyType_GetSlot(tp, Py_tp_alloc);
     if (!alloc) return NULL;
+    /* a snapshot holding a reference to every (connection, datagram) item:
+       the datagram copies below run without the GIL, while another thread
+       may change the caller's list */
+    items = PySequence_Tuple(items);
+    if (!items) return NULL;
 
     PtrMap pm = {0};
     uint32_t *conn_of = NULL, *slot_of = NULL;
@@ -1577,7 +1588,7 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
     size_t total = 0;
     uint32_t nl = 0;  /* packets to launch */
     for (Py_ssize_t i = 0; i < n; ++i) {
-        PyObject *it = PyList_GetItem(items, i);
+        PyObject *it = PyTuple_GetItem(items, i);
         PyObject *c = PyTuple_Check(it) && PyTuple_Size(it) == 2 ? PyTuple_GetItem(it, 0) : NULL;
         PyObject *d = c ? PyTuple_GetItem(it, 1) : NULL;
         if (!d || !PyBytes_Check(d)) goto fallback;
@@ -1621,7 +1632,7 @@ static PyObject *py_receive_short(PyObject *m, PyObject *args)
         qpp_session *ss = session();
         if (!ss || check_rc(qpp_session_stage(ss, total ? total : 1, nl, &hin, &hout)) < 0) goto done;
         for (uint32_t k = 0; k < nl; ++k) cd[k] = hin + desc[k].in_off;
-        Py_BEGIN_ALLOW_THREADS  /* `items` holds every datagram */
+        Py_BEGIN_ALLOW_THREADS  /* the snapshot holds every datagram */
         par_copy(cd, cs, cl, nl, total);
         Py_END_ALLOW_THREADS
         if (host_call(0, kt, desc, nl, hin, total, hout, total, PyBytes_AsString(res)) < 0) goto done;
@@ -1718,6 +1729,7 @@ done:
     ptrmap_free(&pm);
     free(conn_of), free(slot_of), free(desc), free(cd), free(cs), free(cl), free(blocked_pair), free(blocked_space);
     free(blocked_conn), free(od), free(os_), free(ol);
+    Py_DECREF(items);
     Py_XDECREF(closed_out);
     Py_XDECREF(s_rsv);
     Py_XDECREF(s_closed);
@@ -1770,6 +1782,15 @@ static PyObject *py_abi(PyObject *m, PyObject *unused)
     return PyLong_FromLong(qpp_abi_version());
 }
 
+static PyObject *py_watchdog(PyObject *m, PyObject *unused)
+{
+    uint32_t v;
+    Py_BEGIN_ALLOW_THREADS
+    v = qpp_watchdog_count();
+    Py_END_ALLOW_THREADS
+    return PyLong_FromUnsignedLong(v);
+}
+
 #ifndef QPP_SOURCE_HASH
 #error "build with -DQPP_SOURCE_HASH (aioquic_amd/build.py)"
 #endif
@@ -1805,6 +1826,7 @@ static PyMethodDef module_methods[] = {
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},
+    {"watchdog_count", py_watchdog, METH_NOARGS, "GCM table-entry watchdog events on the current device (0 expected)"},
     {"source_hash", py_source_hash, METH_NOARGS, "hash of the native sources this module was built from"},
     {NULL},
 };

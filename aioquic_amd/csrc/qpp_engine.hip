@@ -1143,6 +1143,10 @@ template <int WG>
 constexpr int gcm_tab_entries() { return WG == 512 ? 1 : kTabEntries; }
 static_assert(kGhLdsEntry % 1024 == 0, "LDS-DMA pieces of 1 KiB");
 
+// GCM table-entry watchdog events since the library loaded (tab_acquire gave
+// up: that slot's packets were skipped without results); never expected.
+__device__ uint32_t g_qpp_watchdog;
+
 template <int WG, int NE = gcm_tab_entries<WG>()>
 struct __attribute__((aligned(16))) GcmSmem {
     // GHASH table entries first (LDS offset 0: the entry's offset rides in
@@ -1162,7 +1166,10 @@ struct __attribute__((aligned(16))) GcmSmem {
 
 // Entry of slot `cur` for the calling wave (wave-uniform control flow):
 // found, or loaded into a free entry.  Lane 0 does the bookkeeping under the
-// workgroup's LDS lock.  Returns once the entry's table is in LDS.
+// workgroup's LDS lock.  Returns once the entry's table is in LDS.  (Returning
+// before the table has landed, to overlap its LDS-DMA with the packets'
+// descriptors and headers, measured 2-4 % slower at 64 Ki: those loads queue
+// behind the DMA in the vector memory counter, profiles/r4d_ab_tab_defer.txt.)
 template <int WG>
 __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t cur)
 {
@@ -1424,7 +1431,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     if (lane_fresh() == 0) lds_st(&sm.wslot[wv], kNoSlot);
                 }
                 const uint32_t e = tab_acquire<WG>(sm, gtab, cur);
-                if (e == kNoSlot) continue;
+                if (e == kNoSlot) {
+                    // the watchdog gave up: the slot's packets are not
+                    // processed.  Their results are not written (per-packet
+                    // reporting here costs the step loop registers), so the
+                    // launch counts the event for the host to read
+                    // (qpp_watchdog_count; the GPU test suite checks it).
+                    if (lane_fresh() == 0) atomicAdd(&g_qpp_watchdog, 1u);
+                    continue;
+                }
                 if (lane_fresh() == 0) {
                     lds_st(&sm.wslot[wv], cur);
                     lds_st(&sm.went[wv], e);
@@ -1801,6 +1816,16 @@ extern "C" {
 
 int qpp_abi_version(void) { return QPP_ABI_VERSION; }
 
+uint32_t qpp_watchdog_count(void)
+{
+    uint32_t v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_qpp_watchdog), sizeof v, 0, hipMemcpyDeviceToHost) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return v;
+}
+
 const char *qpp_strerror(int rc)
 {
     switch (rc) {
@@ -2002,7 +2027,10 @@ static uint32_t gcm_grid(uint32_t items, uint32_t waves_per_wg)
 // two workgroups sharing a CU do not progress at the same rate, so over many
 // items per wave one ends well before the other; and each holds one GHASH
 // table entry.  So: two per CU when the table holds one key of the suite and
-// the launch has at most one item per wave.
+// the launch has at most one item per wave.  (Round 4: two per CU for every
+// single-key launch, its waves drawing pooled chunks of 8 items from a
+// launch-wide counter fetched ahead of need, measured no faster than one of
+// 1024 at the north star, profiles/r4f_ab_pooled.txt.)
 static bool gcm_two_wg(const qpp_keytab *kt, uint32_t suite, uint32_t items)
 {
     return kt->n_suite[suite] == 1 && items <= cu_count() * 16u;  // 2 workgroups x 8 waves per CU
@@ -2621,13 +2649,21 @@ static int multi_run(bool enc, qpp_multi *m, const qpp_desc *desc, uint32_t n, c
         }
         if (x.ilo == SIZE_MAX) x.ilo = x.ihi = x.olo = x.ohi = 0;
     }
-    // ranges in output order with disjoint extents, or one device
-    for (int k = 1; k < parts; ++k)
-        if (r[k].ohi > r[k].olo && r[k - 1].ohi > r[k].olo) {
+    // ranges in output order with disjoint extents, or one device: every
+    // non-empty range starts at or after the end of all earlier non-empty
+    // ones (an empty range -- every packet rejected -- compares with nothing)
+    size_t seen_hi = 0;
+    bool seen = false;
+    for (int k = 0; k < parts; ++k) {
+        if (r[k].ohi <= r[k].olo) continue;
+        if (seen && seen_hi > r[k].olo) {
             parts = 1;
             r.assign(1, Range{0, n, 0, in_len, 0, out_len});
             break;
         }
+        seen_hi = std::max(seen_hi, r[k].ohi);
+        seen = true;
+    }
     if (parts == 1) {
         int prev = 0;
         (void)hipGetDevice(&prev);

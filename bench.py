@@ -13,8 +13,13 @@ step buckets each batch by (suite, key) on the device (qpp_plan_build)
 inside the timed region, once for the protect batch and once for the
 unprotect batch.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ns] [--e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ns] [--no-e2e]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+After the timed region rank 0 also times the path the north star says
+starts and ends in host memory (UDP socket buffers): pinned H2D -> protect ->
+unprotect -> D2H on its own 1Mi-packet workload, reported as "e2e" beside
+`value` and never as `value` (--no-e2e skips it).
 
 --gpus N without a launcher (WORLD_SIZE unset) starts N rank processes
 itself, one per visible GPU, before anything touches a GPU; with fewer than N
@@ -78,9 +83,13 @@ def parse():
                     help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-all-cores", type=int, default=1,
                     help="also time the reference on every host core of this GPU's share")
-    ap.add_argument("--event-every", type=int, default=10,
-                    help="bracket the kernels of every N-th timed step with HIP events (1 = all)")
-    ap.add_argument("--e2e", action="store_true", help="also time pinned H2D->kernels->D2H")
+    ap.add_argument("--event-every", type=int, default=1,
+                    help="bracket the kernels of every N-th timed step (steps N-1, 2N-1, ...) with HIP "
+                         "events (1 = all, the default: the kernels' event intervals then lie inside the "
+                         "timed steps, so they sum to at most ms_per_step)")
+    ap.add_argument("--e2e", dest="e2e", action="store_true", default=True,
+                    help="time pinned H2D->kernels->D2H after the timed region (the default)")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false", help="skip the end-to-end leg")
     ap.add_argument("--e2e-packets", type=int, default=1 << 20,
                     help="packets of the end-to-end run (the north star's 1Mi)")
     ap.add_argument("--e2e-chunks", type=int, default=32)
@@ -384,7 +393,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")
+        # gloo reports its connections on the C++ side's stdout: keep them out
+        # of the one JSON line (fd 1 -> fd 2 while the group forms)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     cfg = dict(CONFIGS[args.config])
     if args.keys:
         cfg["n_keys"] = args.keys
@@ -439,17 +457,18 @@ def main():
     def step(ev=None):
         # bucketed configs: each batch is sorted by (suite, key) on the device
         # first -- the protect batch and the unprotect batch each get their own
-        # plan build, as two independent batches of a server would
+        # plan build, as two independent batches of a server would.  Unbucketed
+        # steps record 3 events (ev[1] / ev[3] alias ev[0] / ev[2] then).
         if ev:
             hev.record(ev[0], stream)
         plan = eng.bucket(d_desc, n, stream) if bucketed else None
-        if ev:
+        if ev and bucketed:
             hev.record(ev[1], stream)
         eng.protect(d_desc, n, d_plain, d_wire, d_r1, stream, plan)
         if ev:
             hev.record(ev[2], stream)
         plan = eng.bucket(d_udesc, n, stream) if bucketed else None
-        if ev:
+        if ev and bucketed:
             hev.record(ev[3], stream)
         eng.unprotect(d_udesc, n, d_wire, d_back, d_r2, stream, plan)
         if ev:
@@ -464,7 +483,15 @@ def main():
     # for the roofline).  Sampling keeps the events' own stream time (a few us
     # per record) out of most steps of `value`.
     every = max(1, args.event_every)
-    evs = [[hev.new() for _ in range(5)] if k % every == 0 else None for k in range(args.steps)]
+    # (sampled: not the first timed step, which follows the barrier, the
+    # others follow a step)
+    def new_evs():
+        e = [hev.new() for _ in range(5 if bucketed else 3)]
+        return e if bucketed else [e[0], e[0], e[1], e[1], e[2]]
+
+    evs = [new_evs() if k % every == every - 1 else None for k in range(args.steps)]
+    if not any(evs):
+        evs[-1] = new_evs()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

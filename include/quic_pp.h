@@ -135,6 +135,11 @@ int qpp_abi_version(void);
 /* 16 hex digits: the hash of the native sources the library was built from
  * (aioquic_amd/_srchash.py); a binding checks it against its own at load. */
 const char *qpp_source_hash(void);
+/* GCM table-entry watchdog events on the current device since the library
+ * loaded: a launch whose kernel waited ~1 s for a GHASH table entry skipped
+ * that key slot's packets without writing their results.  Never expected
+ * (it would be a bug); tests check it stays 0.  A synchronous read. */
+uint32_t qpp_watchdog_count(void);
 const char *qpp_strerror(int rc);
 int qpp_device_check(void);             /* QPP_OK if the current device is gfx950 */
 

@@ -60,3 +60,11 @@ def test_shape_boundary_one_key(oracle):
     recs = _keys(np.random.default_rng(51), 1, suites=(0,))
     _check(oracle, recs, 4096 * 16 + 16, 61, max_payload=64)
     _check(oracle, recs, 4096 * 16, 62, max_payload=64)
+
+
+
+def test_one_key_many_items(oracle):
+    """One key, 12,300 items of small packets (about 3 items per wave on a
+    256-CU part, one 1024-thread workgroup per CU) with a ragged last item."""
+    recs = _keys(np.random.default_rng(71), 1, suites=(0,))
+    _check(oracle, recs, 12300 * 16 - 5, 72, max_payload=48)

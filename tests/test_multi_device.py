@@ -82,3 +82,25 @@ def test_multi_into_caller_buffers():
     res2 = np.zeros(len(w.desc), L.RESULT)
     multi.unprotect_into(w.udesc, out, back, res2)
     assert (res2["status"] == 0).all() and np.array_equal(back, w.plain)
+
+
+def test_multi_empty_middle_range_out_of_order():
+    """A middle range whose packets are all rejected has no extent: the
+    ranges around it must still be checked against each other.
+    Descriptors by thirds in reverse output order, the middle third rejected:
+    the outer ranges' extents are out of order, so the batch runs on one
+    device, byte for byte as one session."""
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import MultiDeviceEngine, PacketEngine
+
+    w = _workload(900, 0x54)
+    one = PacketEngine(w.n_keys)
+    one.set_key_records(w.keys)
+    multi = MultiDeviceEngine(w.n_keys, devices=[0, 0, 0])
+    multi.set_key_records(w.keys)
+    d = np.concatenate([w.desc[600:], w.desc[300:600], w.desc[:300]]).copy()
+    d["in_off"][300:600] = w.plain_size + 1  # every packet of range 1 rejected
+    a = one.protect_host(d, w.plain, w.wire_size)
+    b = multi.protect_host(d, w.plain, w.wire_size)
+    assert (a[1]["status"][300:600] == L.S_LENGTH).all() and (a[1]["status"][:300] == L.S_OK).all()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])

@@ -360,3 +360,28 @@ def test_key_slots_release_on_teardown_and_update():
     w = sb.flush()
     assert len(w) == 1 and not any(k[0] == id(old) for k in slots._slot)
     assert len(slots._keep) == 1
+
+
+@pytest.mark.gpu
+def test_key_release_from_another_thread_is_queued():
+    """A context torn down on another thread does not touch this thread's
+    table there and then: the release is queued and applied at the
+    table's next assign(), by its own thread."""
+    import threading
+
+    from aioquic_amd.batch_io import KeySlots, SendBatch
+    from aioquic_amd.crypto import CryptoPair
+
+    p = CryptoPair()
+    p.setup_initial(bytes(8), is_client=True, version=QuicProtocolVersion.VERSION_1)
+    slots = KeySlots(8)
+    sb = SendBatch(slots)
+    sb.add(p, bytes([0x41]) + bytes(8) + bytes(2), bytes(40), 0)
+    sb.flush()
+    assert len(slots._keep) == 1
+    t = threading.Thread(target=p.teardown)
+    t.start()
+    t.join()
+    assert len(slots._keep) == 1 and slots._inbox  # queued (recv and send), not applied
+    slots.assign([])
+    assert len(slots._keep) == 0 and not slots._inbox and not slots._by_obj
