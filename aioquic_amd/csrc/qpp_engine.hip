@@ -59,11 +59,14 @@ constexpr int kChachaWpe = 4;
 constexpr int kChRegion = 64 * 16 + 16;
 constexpr int kChStage = 4 * kChRegion;
 
+// pw entries: 1, r, r^2 .. r^5, r^8
+constexpr int kPwOne = 0, kPw1 = 1, kPw8 = 6, kPwEntries = 7;
+
 template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
     uint8_t stage[WG / 64][kChStage];
     uint8_t scratch[WG / 4][kScratch];
-    uint32_t pw[WG / 4][20];  // per packet: r, r^2, r^3, r^4 (5 limbs each) for the tag's close
+    uint32_t pw[WG / 4][5 * kPwEntries];  // per packet: the tag close's powers of r (5 limbs each)
 };
 
 // Fill the LDS AES image: row x = [Te0[x] x 32 | Te1[x] x 32], 16-byte stores.
@@ -854,6 +857,26 @@ __device__ __forceinline__ P130 launder(P130 x)
     return x;
 }
 
+// lane J's value in every lane of the quad (DPP quad_perm [J,J,J,J])
+template <int J>
+__device__ __forceinline__ P130 p130_from_lane(P130 x)
+{
+#pragma unroll
+    for (int l = 0; l < 5; ++l) x.v[l] = quad_dpp<J * 0x55>(x.v[l]);
+    return x;
+}
+
+// limb-wise sum over the quad, in every lane (no carries: 4 limbs of < 2^27)
+__device__ __forceinline__ P130 p130_quad_sum(P130 x)
+{
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        x.v[l] += quad_dpp<0xB1>(x.v[l]);
+        x.v[l] += quad_dpp<0x4E>(x.v[l]);
+    }
+    return x;
+}
+
 // 16 bytes per lane from buffer offset `off` (out of range: zeros) into LDS at
 // lds + 16 * lane (LDS-DMA)
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *lds, uint32_t off)
@@ -1000,16 +1023,25 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         for (int w = 0; w < 8; ++w) kw[w] = quad_dpp<0x00>(blk[w]);
         *(u32x4 *)(scr + kScrEj0) = u32x4{kw[4], kw[5], kw[6], kw[7]};
         r = p130_r(kw[0], kw[1], kw[2], kw[3]);
-        const P130 r2 = p130_mul(r, r), r4 = p130_mul(r2, r2);
-        r13 = p130_mul(p130_mul(p130_mul(r4, r4), r4), r);
-        if (sub == 0) {
-            const P130 r3 = p130_mul(r2, r);
+        // powers, lane-parallel: r^2; lane 0 r^3 beside lane 1 r^4; lane 0
+        // r^5 beside lane 1 r^8; r^13 = r^8 r^5 -- 4 multiplies per lane
+        // instead of 5 plus lane 0's r^3
+        const P130 r2 = p130_mul(r, r);
+        const P130 b34 = p130_mul(r2, sub == 0 ? r : r2);
+        const P130 r3 = p130_from_lane<0>(b34), r4 = p130_from_lane<1>(b34);
+        const P130 b58 = p130_mul(r4, sub == 0 ? r : r4);
+        const P130 r5 = p130_from_lane<0>(b58), r8 = p130_from_lane<1>(b58);
+        r13 = p130_mul(r8, r5);
+        if (sub == 0) {  // the close's powers (kPwOne .. kPw8)
 #pragma unroll
             for (int l = 0; l < 5; ++l) {
-                pw[l] = r.v[l];
-                pw[5 + l] = r2.v[l];
-                pw[10 + l] = r3.v[l];
-                pw[15 + l] = r4.v[l];
+                pw[5 * kPwOne + l] = l == 0 ? 1u : 0u;
+                pw[5 * kPw1 + l] = r.v[l];
+                pw[5 * (kPw1 + 1) + l] = r2.v[l];
+                pw[5 * (kPw1 + 2) + l] = r3.v[l];
+                pw[5 * (kPw1 + 3) + l] = r4.v[l];
+                pw[5 * (kPw1 + 4) + l] = r5.v[l];
+                pw[5 * kPw8 + l] = r8.v[l];
             }
         }
         // lane 0 starts its chain with the associated data (its next chunk,
@@ -1049,40 +1081,40 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         uint8_t *dst = P.dst;
         P = unpark(scr, src, dst, !ENC);
     }
-    // Close the four chains in one Horner pass over the quad.  Lane j's chain
-    // ends at the last block of its last chunk (lane 0 without a chunk: the
-    // last header block, position -1); the lanes' ends follow one another in
-    // the order L + 1, L + 2, L + 3, L (mod 4), L = chunks mod 4 holding the
-    // final chunk, 4 blocks apart except the final chunk's nb blocks:
-    //   S = ((A[L+1] r^4 + A[L+2]) r^4 + A[L+3]) r^nb + A[L]
-    // (a lane with no block at all holds 0).  Every lane computes S from the
-    // quad's chains exchanged through the (now idle) staging regions and the
-    // packet's r^2..r^4 parked in LDS at the key block.
-    {
-        uint8_t *q0 = stage + qoff, *q1 = stage + kChRegion + qoff;
-        *(u32x4 *)(q0 + 16 * sub) = u32x4{acc.v[0], acc.v[1], acc.v[2], acc.v[3]};
-        *(uint32_t *)(q1 + 4 * sub) = acc.v[4];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-    }
-    auto chain = [&](int j) -> P130 {
-        const u32x4 v = *(const u32x4 *)(stage + qoff + 16 * (j & 3));
-        return P130{{v.x, v.y, v.z, v.w, *(const uint32_t *)(stage + kChRegion + qoff + 4 * (j & 3))}};
-    };
-    auto power = [&](int e) -> P130 {  // r^e, e = 1..4
-        P130 x;
-#pragma unroll
-        for (int l = 0; l < 5; ++l) x.v[l] = pw[5 * (e - 1) + l];
-        return x;
-    };
+    // Close the four chains.  Lane j's chain ends at the last block of its
+    // last chunk (lane 0 without a chunk: the last header block, position
+    // -1); the lanes' ends follow one another in the order L + 1, L + 2,
+    // L + 3, L (mod 4), L = chunks mod 4 holding the final chunk, 4 blocks
+    // apart except the final chunk's nb blocks (a lane with no block at all
+    // holds 0), and the lengths block follows, so the tag's polynomial is
+    //   A[L+1] r^(9+nb) + A[L+2] r^(5+nb) + A[L+3] r^(1+nb) + (A[L] + lens) r
+    //   = (A[L+1] r^8 + A[L+2] r^4 + A[L+3]) r^(nb+1) + (A[L] + lens) r.
+    // Two multiplies per lane: each lane's own chain by its role's power
+    // (r^8, r^4, 1, r: pw entries parked at the key block), two quad sums,
+    // then the first sum by r^(nb+1) -- instead of a 4-multiply Horner pass
+    // over chains exchanged through LDS.
     const int L = chunks & 3;
     const int nb = chunks > 0 ? n_c - 4 * (chunks - 1) : 1;
-    const P130 r4 = power(4);
-    P130 sum = p130_add(p130_mul(chain(L + 1), r4), chain(L + 2));
-    sum = p130_add(p130_mul(sum, r4), chain(L + 3));
-    sum = p130_add(p130_mul(sum, power(nb)), chain(L));
+    const int role = (sub - L - 1) & 3;  // 0: lane L+1, 1: L+2, 2: L+3, 3: L
+    auto power = [&](int e) -> P130 {    // pw entry e
+        P130 x;
+#pragma unroll
+        for (int l = 0; l < 5; ++l) x.v[l] = pw[5 * e + l];
+        return x;
+    };
     const u32x4 lens = u32x4{(uint32_t)P.hlen, 0u, (uint32_t)P.clen, 0u};
-    sum = p130_mul(p130_add(sum, p130_block(lens)), power(1));
+    const P130 lb = p130_block(lens);
+    P130 a = acc;
+#pragma unroll
+    for (int l = 0; l < 5; ++l) a.v[l] += role == 3 ? lb.v[l] : 0u;
+    const P130 m = p130_mul(a, power(role == 0 ? kPw8 : role == 1 ? kPw1 + 3 : role == 2 ? kPwOne : kPw1));
+    P130 u = m, v = p130_zero();
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        u.v[l] = role == 3 ? 0u : m.v[l];
+        v.v[l] = role == 3 ? m.v[l] : 0u;
+    }
+    const P130 sum = p130_add(p130_mul(p130_quad_sum(u), power(kPw1 + nb)), p130_quad_sum(v));
     const u32x4 sw = *(const u32x4 *)(scr + kScrEj0);
     const u32x4 tag = p130_finish(sum, sw.x, sw.y, sw.z, sw.w);
     if (ENC) {

@@ -1,0 +1,78 @@
+"""Whole-batch checker built on the reference's own per-packet path.
+
+oracle/_ref/aioquic_ref/_crypto*.so is /root/reference/src/aioquic/_crypto.c
+compiled by `make -C oracle ref` against the system libcrypto (never part of
+the package; it travels to the GPU box as a built file, the reference source
+does not).  Test infrastructure only: the packets of a bench_data workload go
+through AEAD.encrypt + HeaderProtection.apply and HeaderProtection.remove +
+decode_packet_number + AEAD.decrypt one by one, exactly as
+quic/crypto.py:75-116 drives them, at ~1-3 us per packet, so a 1 Mi batch is
+checked whole in seconds where the plain-C restatement (oracle/qpp_oracle.c,
+bitwise GHASH) would take minutes.
+"""
+
+import glob
+import importlib.util
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_NAMES = {0: (b"aes-128-gcm", b"aes-128-ecb", 16), 1: (b"aes-256-gcm", b"aes-256-ecb", 32),
+          2: (b"chacha20-poly1305", b"chacha20", 32)}
+
+
+def load():
+    """The reference's _crypto module, or None when oracle/_ref is not built."""
+    so = glob.glob(os.path.join(ROOT, "oracle", "_ref", "aioquic_ref", "_crypto*.so"))
+    if not so:
+        return None
+    spec = importlib.util.spec_from_file_location("_crypto", so[0])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _objects(ref, keys):
+    objs = []
+    for k in keys:
+        an, hn, kl = _NAMES[int(k["suite"])]
+        objs.append((ref.AEAD(an, bytes(k["key"][:kl]), bytes(k["iv"])),
+                     ref.HeaderProtection(hn, bytes(k["hp"][:kl]))))
+    return objs
+
+
+def protect_all(ref, w) -> np.ndarray:
+    """The wire image of every packet of workload w (bench_data layout:
+    dense 1200-byte slots, header at in_off, payload after it)."""
+    objs = _objects(ref, w.keys)
+    out = np.zeros(w.wire_size, np.uint8)
+    buf = w.plain.tobytes()
+    for d in w.desc:
+        i, o, h, n = int(d["in_off"]), int(d["out_off"]), int(d["hdr_len"]), int(d["len"])
+        aead, hp = objs[int(d["slot"])]
+        hdr = buf[i : i + h]
+        pkt = hp.apply(hdr, aead.encrypt(buf[i + h : i + h + n], hdr, int(d["pn"])))
+        out[o : o + len(pkt)] = np.frombuffer(pkt, np.uint8)
+    return out
+
+
+def unprotect_all(ref, w, wire: np.ndarray):
+    """(plaintext image, decoded packet numbers) of every packet of w's wire
+    image; a failed packet raises (the batch is expected to authenticate)."""
+    from aioquic_amd.packet import decode_packet_number
+
+    objs = _objects(ref, w.keys)
+    out = np.zeros(w.plain_size, np.uint8)
+    pns = np.zeros(len(w.udesc), np.uint64)
+    buf = wire.tobytes()
+    for j, d in enumerate(w.udesc):
+        i, o, n, pn_off = int(d["in_off"]), int(d["out_off"]), int(d["len"]), int(d["hdr_len"])
+        aead, hp = objs[int(d["slot"])]
+        hdr, trunc = hp.remove(buf[i : i + n], pn_off)
+        pn = decode_packet_number(trunc, ((hdr[0] & 3) + 1) * 8, int(d["pn"]))
+        pt = aead.decrypt(buf[i + len(hdr) : i + n], hdr, pn)
+        out[o : o + len(hdr)] = np.frombuffer(hdr, np.uint8)
+        out[o + len(hdr) : o + len(hdr) + len(pt)] = np.frombuffer(pt, np.uint8)
+        pns[j] = pn
+    return out, pns

@@ -103,3 +103,26 @@ def test_oracle_against_reference_golden(oracle):
         assert exp["ok"], c["seed"]
         assert h.hex() == exp["header"] and pn == exp["pn"] and matches(exp["payload"], p)
         assert first is not None
+
+
+@pytest.mark.parametrize("suite", [0, 1, 2])
+def test_reference_batch_checker_matches_oracle(oracle, suite):
+    """tests/ref_crypto.py (the reference's own _crypto over a whole batch, the
+    full-size GPU tests' checker) agrees with the C oracle packet for packet."""
+    import numpy as np
+
+    from aioquic_amd import bench_data
+    from tests import ref_crypto
+
+    ref = ref_crypto.load()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (make -C oracle ref)")
+    w = bench_data.make_workload(256, suite=suite, n_keys=3, seed=0x77 + suite, order="random")
+    wire = ref_crypto.protect_all(ref, w)
+    o_wire, o_res = oracle.protect_batch(w.keys, w.desc, w.plain, w.wire_size)
+    assert (o_res["status"] == 0).all()
+    assert np.array_equal(wire, o_wire)
+    back, pns = ref_crypto.unprotect_all(ref, w, wire)
+    o_back, o_res2 = oracle.unprotect_batch(w.keys, w.udesc, wire, w.plain_size)
+    assert np.array_equal(back, o_back) and np.array_equal(back, w.plain)
+    assert np.array_equal(pns, o_res2["pn"]) and np.array_equal(pns, w.desc["pn"])
