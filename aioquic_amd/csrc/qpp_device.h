@@ -92,7 +92,11 @@ constexpr int kGh5Windows = 26;
 constexpr int kGh5Hi = 27 * 256;  // offset of the high halves
 constexpr int kGh5Bytes = 14 * 1024;
 constexpr int kGh5Off = kGhashPowers * kGhashPowBytes;  // offset of the 5-bit H^4 in a slot's tables
-constexpr int kGhashTabBytes = kGh5Off + kGh5Bytes;      // 46 KiB per slot
+// H^1 .. H^kGhPowCount as plain 16-byte elements, for the lone-packet kernel
+// (k_lone: GHASH as sum_i X_i H^(m-i) over a packet's m <= 189 blocks)
+constexpr int kGhPowCount = 192;
+constexpr int kGhPowOff = kGh5Off + kGh5Bytes;
+constexpr int kGhashTabBytes = kGhPowOff + kGhPowCount * 16;  // 49 KiB per slot
 // one LDS table entry of the GCM kernel: H^4 in the step loop's layout
 constexpr int kGhLdsEntry = kGh5Bytes;
 

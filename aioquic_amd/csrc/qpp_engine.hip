@@ -1596,6 +1596,279 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
     }
 }
 
+// ----------------------------------------------------------- lone packets --
+//
+// A launch of a few packets -- the object API, one packet per call
+// (AEAD.encrypt / decrypt, _crypto.c:157-194 / :115-155, through
+// CryptoContext, quic/crypto.py:75-116) -- is bound by latency, not by
+// throughput: the quad kernels walk a 1200-byte packet in ~10 dependent steps
+// (k_gcm: ~38 us for one packet, profiles/r3o_latency).  Here one wave takes
+// one packet and all of its blocks at once: AES-GCM gives every lane 1-3 of
+// the packet's 16-byte blocks, ChaCha20-Poly1305 one 64-byte chunk (or 4
+// blocks of associated data).  The authenticator is then
+//   sum_i X_i K^(m - i)   over the m blocks [AAD | CT | lengths],
+// each lane multiplying its blocks by their own power of K (H^e from the
+// slot's power table, r^e by square-and-multiply), and one wave reduction.
+constexpr int kLoneWG = 1024;      // 16 packets per workgroup, one AES image
+constexpr uint32_t kLoneMax = 16;  // unplanned launches of at most this many packets
+
+__device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v)
+{
+    v ^= dpp_mov<kDppQuadSwap1>(v);
+    v ^= dpp_mov<kDppQuadSwap2>(v);
+    v ^= dpp_mov<kDppHalfMirror>(v);
+    v ^= dpp_mov<kDppMirror>(v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 16) ^
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+    v += dpp_mov<kDppQuadSwap1>(v);
+    v += dpp_mov<kDppQuadSwap2>(v);
+    v += dpp_mov<kDppHalfMirror>(v);
+    v += dpp_mov<kDppMirror>(v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+__device__ __forceinline__ u32x4 readlane4(u32x4 v, int l)
+{
+    return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, l), (uint32_t)__builtin_amdgcn_readlane((int)v.y, l),
+                 (uint32_t)__builtin_amdgcn_readlane((int)v.z, l), (uint32_t)__builtin_amdgcn_readlane((int)v.w, l)};
+}
+
+// The packet's slot for a lone-packet launch of SUITE, as the quad kernels
+// decide it: beyond the table or empty -> KeyUnavailableError (written by
+// every suite's launch alike), another suite -> that suite's launch.
+template <int SUITE>
+__device__ __forceinline__ bool lone_slot(const qpp_desc &d, const KeySlot *slots, uint32_t cap,
+                                          qpp_result *res, uint32_t p)
+{
+    bool none = d.slot >= cap;
+    if (!none) {
+        const uint32_t suite = __builtin_amdgcn_readfirstlane(slots[d.slot].suite);
+        if (suite != (uint32_t)SUITE) {
+            if (suite <= QPP_CHACHA20_POLY1305) return false;
+            none = true;
+        }
+    }
+    if (none) {
+        if (lane_fresh() == 0) res[p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+        return false;
+    }
+    return true;
+}
+
+// Protect with header protection: the sample from ct[0, 32) staged by the
+// lanes of CT blocks 0 and 1 (and the tag, for ciphertexts under 32 bytes),
+// the mask by every quad, the header out by the lanes of its blocks.
+template <int SUITE, class TE>
+__device__ __forceinline__ void lone_protect_hp(Pkt &P, const KeySlot *ks, uint8_t *scr, u32x4 tag,
+                                                const TE &T)
+{
+    const uint32_t lane = lane_fresh();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (P.clen < 32 && lane == 0)
+        for (int j = 0; j < 16 && P.clen + j < 32; ++j) scr[P.clen + j] = (uint8_t)byte_of(tag, j);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    P.mask = hp_mask_quad<SUITE>(ks, lds_sample(scr, 4 - P.pn_len), T, (int)(lane & 3));
+    const int n_a = (P.hlen + 15) >> 4;
+    for (int q = (int)lane; q < n_a; q += 64) {
+        const int nb = min(16, P.hlen - 16 * q);
+        u32x4 h = ld_win(P.src + 16 * q, nb, P.src, P.src + P.hlen + P.clen);
+        h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
+        st_part(P.dst + 16 * q, h, nb);
+    }
+}
+
+// One AES-GCM packet per wave (SP 800-38D; _crypto.c:157-204 / :115-155).
+template <int SUITE, bool ENC>
+__global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict__ slots,
+                                                      const uint8_t *__restrict__ gtab, uint32_t cap,
+                                                      const qpp_desc *__restrict__ desc, uint32_t n,
+                                                      const uint8_t *gin, uint8_t *gout,
+                                                      qpp_result *__restrict__ res)
+{
+    constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
+    __shared__ __attribute__((aligned(16))) uint8_t te[kTeBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t scr[kLoneWG / 64][48];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
+    load_te<kLoneWG>(te);
+    __syncthreads();
+    if (p >= n) return;
+    const qpp_desc d = desc[p];
+    if (!lone_slot<SUITE>(d, slots, cap, res, p)) return;
+    const KeySlot *ks = slots + d.slot;
+    const uint32_t lane = lane_fresh();
+    const LdsTe T{te, (lane & 31) * 4};
+    const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
+    Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
+    if (P.status == QPP_S_OK) {
+        uint32_t rk[4 * (kNR + 1)];
+#pragma unroll
+        for (int i = 0; i < 4 * (kNR + 1); ++i)
+            rk[i] = __builtin_amdgcn_readfirstlane((i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
+        const CtrCache cc = ctr_cache(P.nonce, rk, T);
+        const int hlen = P.hlen, clen = P.clen;
+        const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, m = n_a + n_c + 1;
+        const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
+        const uint8_t *src = P.src;
+        uint8_t *dst = P.dst;
+        const uint8_t *hpw = gtab + (size_t)d.slot * kGhashTabBytes + kGhPowOff;
+        const bool masked = !ENC && P.hp;
+        // sequence position pos = lane + 64 k: AAD block, CT block or the
+        // lengths block; its GHASH term X_pos H^(m - pos)
+        u32x4 y = zero4(), ej0 = zero4();
+        for (int k = 0; k < 3; ++k) {
+            const int pos = (int)lane + 64 * k;
+            if (pos >= m) break;
+            u32x4 x;
+            if (pos < n_a) {
+                const int nb = min(16, hlen - 16 * pos);
+                x = ld_win(src + 16 * pos, nb, src, src + rlen);
+                if (masked) x ^= hp_pattern(16 * pos, P.mask, P.fbm, P.pn_off, P.pn_len);
+                if (!ENC || !P.hp) st_part(dst + 16 * pos, x, nb);
+            } else if (pos < n_a + n_c) {
+                const int i = pos - n_a, nb = min(16, clen - 16 * i);
+                const u32x4 in = ld_win(src + hlen + 16 * i, nb, src, src + rlen);
+                const u32x4 o = in ^ aes_ctr<kNR>(cc, (uint32_t)(i + 2), rk, T);
+                st_part(dst + hlen + 16 * i, o, nb);
+                x = keep_bytes(ENC ? o : in, nb);
+                if (ENC && P.hp && i < 2) *(u32x4 *)(scr[wv] + 16 * i) = x;
+            } else {
+                x = u32x4{0u, bswap((uint32_t)hlen * 8u), 0u, bswap((uint32_t)clen * 8u)};
+                ej0 = aes_ctr<kNR>(cc, 1u, rk, T);
+            }
+            y ^= gf128_mul_slow(x, ld16(hpw + 16 * (m - 1 - pos)));
+        }
+        const u32x4 tag = u32x4{wave_xor_u32(y.x), wave_xor_u32(y.y), wave_xor_u32(y.z), wave_xor_u32(y.w)} ^
+                          readlane4(ej0, (m - 1) & 63);
+        if (ENC) {
+            if (lane == 0) st16(dst + hlen + clen, tag);
+            if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[wv], tag, T);
+        } else {
+            const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
+            if ((diff.x | diff.y | diff.z | diff.w) != 0) {
+                P.status = QPP_S_DECRYPT;
+                for (int k = 0; k < 3; ++k) {
+                    const int i = (int)lane + 64 * k - n_a;
+                    if (i >= 0 && i < n_c) st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
+                }
+            }
+        }
+    }
+    write_result<ENC>(res, p, (int)lane_fresh(), P);
+}
+
+// One ChaCha20-Poly1305 packet per wave (RFC 8439 sec. 2.8).  Lane 0: the
+// one-time key block; lane u = 1..24: chunk u - 1 (4 CT blocks); lane 32 + g:
+// AAD blocks 4g..4g+3; lane 63: the lengths block.  Each lane folds its
+// blocks by Horner in r and scales the result by r^e, e = m - (position of
+// its last block); the 26-bit limbs of <= 49 terms sum without carries.
+template <bool ENC>
+__global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restrict__ slots, uint32_t cap,
+                                                         const qpp_desc *__restrict__ desc, uint32_t n,
+                                                         const uint8_t *gin, uint8_t *gout,
+                                                         qpp_result *__restrict__ res)
+{
+    constexpr int SUITE = QPP_CHACHA20_POLY1305;
+    __shared__ __attribute__((aligned(16))) uint8_t scr[kLoneWG / 64][48];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
+    if (p >= n) return;
+    const qpp_desc d = desc[p];
+    if (!lone_slot<SUITE>(d, slots, cap, res, p)) return;
+    const KeySlot *ks = slots + d.slot;
+    const uint32_t lane = lane_fresh();
+    const ConstTe T;
+    const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
+    Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
+    if (P.status == QPP_S_OK) {
+        const int hlen = P.hlen, clen = P.clen;
+        const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, m = n_a + n_c + 1;
+        const int chunks = (clen + 63) >> 6;
+        const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
+        const uint8_t *src = P.src;
+        uint8_t *dst = P.dst;
+        uint32_t key[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) key[w] = __builtin_amdgcn_readfirstlane(ks->rk[w]);
+        uint32_t blk[16];
+        chacha_block(key, lane, P.nonce.x, P.nonce.y, P.nonce.z, blk);
+        uint32_t kw[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) kw[w] = (uint32_t)__builtin_amdgcn_readlane((int)blk[w], 0);
+        const P130 r = p130_r(kw[0], kw[1], kw[2], kw[3]);
+        // this lane's blocks: first sequence position q, count nb
+        const bool is_ct = lane >= 1 && (int)lane <= chunks;
+        const int g = (int)lane - 32;
+        int q = 0, cnt = 0;
+        if (is_ct) {
+            q = n_a + 4 * ((int)lane - 1);
+            cnt = min(4, n_c - 4 * ((int)lane - 1));
+        } else if (g >= 0 && 4 * g < n_a) {
+            q = 4 * g;
+            cnt = min(4, n_a - 4 * g);
+        } else if (lane == 63) {
+            q = m - 1;
+            cnt = 1;
+        }
+        const bool masked = !ENC && P.hp;
+        P130 w = p130_zero();
+        for (int b = 0; b < cnt; ++b) {
+            u32x4 x;
+            if (is_ct) {
+                const int i = 4 * ((int)lane - 1) + b, nb = min(16, clen - 16 * i);
+                const u32x4 in = ld_win(src + hlen + 16 * i, nb, src, src + rlen);
+                const u32x4 o = in ^ u32x4{blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3]};
+                st_part(dst + hlen + 16 * i, o, nb);
+                x = keep_bytes(ENC ? o : in, nb);
+                if (ENC && P.hp && i < 2) *(u32x4 *)(scr[wv] + 16 * i) = x;
+            } else if (lane == 63) {
+                x = u32x4{(uint32_t)hlen, 0u, (uint32_t)clen, 0u};
+            } else {
+                const int j = 4 * g + b, nb = min(16, hlen - 16 * j);
+                x = ld_win(src + 16 * j, nb, src, src + rlen);
+                if (masked) x ^= hp_pattern(16 * j, P.mask, P.fbm, P.pn_off, P.pn_len);
+                if (!ENC || !P.hp) st_part(dst + 16 * j, x, nb);
+            }
+            w = p130_add(b == 0 ? w : p130_mul(w, r), p130_block(x));
+        }
+        // w r^e, e = m - (q + cnt - 1) (a lane without blocks holds 0)
+        const int e = cnt > 0 ? m - (q + cnt - 1) : 0;
+        P130 rp = r, one = p130_zero();
+        one.v[0] = 1u;
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            w = p130_mul(w, ((e >> bit) & 1) ? rp : one);
+            if (bit < 7) rp = p130_mul(rp, rp);
+        }
+        P130 sum;
+#pragma unroll
+        for (int l = 0; l < 5; ++l) sum.v[l] = wave_sum_u32(w.v[l]);
+        const u32x4 tag = p130_finish(sum, kw[4], kw[5], kw[6], kw[7]);
+        if (ENC) {
+            if (lane == 0) st16(dst + hlen + clen, tag);
+            if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[wv], tag, T);
+        } else {
+            const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
+            if ((diff.x | diff.y | diff.z | diff.w) != 0) {
+                P.status = QPP_S_DECRYPT;
+                if (is_ct)
+                    for (int b = 0; b < cnt; ++b) {
+                        const int i = 4 * ((int)lane - 1) + b;
+                        st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
+                    }
+            }
+        }
+    }
+    write_result<ENC>(res, p, (int)lane_fresh(), P);
+}
+
 // Header-protection masks only (HeaderProtection_mask, _crypto.c:278-287).
 constexpr int kMaskWG = 256;
 
@@ -1693,6 +1966,17 @@ __global__ __launch_bounds__(kSetupWG) void k_key_setup(KeySlot *__restrict__ sl
     for (int i = threadIdx.x; i < (int)(sizeof(KeySlot) / 4); i += kSetupWG)
         ((uint32_t *)dst)[i] = ((const uint32_t *)&ks)[i];
     if (m.suite == QPP_AES_128_GCM || m.suite == QPP_AES_256_GCM) {
+        // H^1 .. H^192 (k_lone) by doubling: H^(h + t + 1) = H^(t + 1) H^h
+        __shared__ u32x4 hall[kGhPowCount];
+        if (threadIdx.x < kGhashPowers) hall[threadIdx.x] = hpow[threadIdx.x];
+        __syncthreads();
+        for (int have = kGhashPowers; have < kGhPowCount; have *= 2) {
+            const int t = threadIdx.x;
+            if (t < have && have + t < kGhPowCount) hall[have + t] = gf128_mul_slow(hall[t], hall[have - 1]);
+            __syncthreads();
+        }
+        u32x4 *hp = (u32x4 *)(gtab + (size_t)m.slot * kGhashTabBytes + kGhPowOff);
+        for (int i = threadIdx.x; i < kGhPowCount; i += kSetupWG) hp[i] = hall[i];
         u32x4 *tab = (u32x4 *)(gtab + (size_t)m.slot * kGhashTabBytes);
         for (int e = threadIdx.x; e < kGhashPowers * 32 * 16; e += kSetupWG) {
             const int p = e >> 9, w = (e >> 4) & 31, v = e & 15;
@@ -2028,6 +2312,18 @@ static int gcm_bpl_choice()
     return b;
 }
 
+// Lone-packet kernels for small unplanned launches (k_lone_gcm /
+// k_lone_chacha); QPP_LONE=0 sends them through the quad kernels instead
+// (a study and test switch, read once per process).
+static bool lone_choice()
+{
+    static const bool b = [] {
+        const char *v = getenv("QPP_LONE");
+        return !(v && v[0] == '0');
+    }();
+    return b;
+}
+
 static uint32_t cu_count()
 {
     static int cus[64];
@@ -2083,6 +2379,33 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     // planned: each suite's launch covers at most every wave item of the batch
     const uint32_t *d_items = plan ? plan->d_items : nullptr, *d_irange = plan ? plan->d_irange : nullptr;
     const uint32_t waves = plan ? qpp_internal_plan_max_items(n, kt->cap) : (n + 15) / 16;
+    if (!plan && n <= kLoneMax && lone_choice()) {
+        // a few packets (the object API): one wave per packet
+        const dim3 grid((n + kLoneWG / 64 - 1) / (kLoneWG / 64)), block(kLoneWG);
+#define QPP_LAUNCH_LONE_GCM(SUITE)                                                                 \
+    if (mask & (1u << SUITE)) {                                                                    \
+        if (enc)                                                                                   \
+            hipLaunchKernelGGL((k_lone_gcm<SUITE, true>), grid, block, 0, s, kt->d_slots, kt->d_gtab, \
+                               kt->cap, d_desc, n, d_in, d_out, d_res);                            \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_lone_gcm<SUITE, false>), grid, block, 0, s, kt->d_slots,           \
+                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);                \
+        HIPCHK(hipGetLastError());                                                                 \
+    }
+        QPP_LAUNCH_LONE_GCM(QPP_AES_128_GCM)
+        QPP_LAUNCH_LONE_GCM(QPP_AES_256_GCM)
+#undef QPP_LAUNCH_LONE_GCM
+        if (mask & (1u << QPP_CHACHA20_POLY1305)) {
+            if (enc)
+                hipLaunchKernelGGL((k_lone_chacha<true>), grid, block, 0, s, kt->d_slots, kt->cap, d_desc, n,
+                                   d_in, d_out, d_res);
+            else
+                hipLaunchKernelGGL((k_lone_chacha<false>), grid, block, 0, s, kt->d_slots, kt->cap, d_desc, n,
+                                   d_in, d_out, d_res);
+            HIPCHK(hipGetLastError());
+        }
+        return QPP_OK;
+    }
     const int bpl_gcm = gcm_bpl_choice();
 #define QPP_LAUNCH_GCM_W(SUITE, BPLV, WGV)                                                     \
     do {                                                                                       \

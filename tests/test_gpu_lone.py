@@ -1,0 +1,232 @@
+"""Lone-packet kernels (k_lone_gcm / k_lone_chacha: one wave per packet, for
+unplanned launches of at most 16 packets -- the object API's one packet per
+call) against the C oracle, chunk by chunk: every suite, short and long
+headers, AEAD-only with associated data up to 1500 bytes, payloads from 0 to
+the 1500-byte limit, tiny inputs, in-place operation, tampered tags and the
+status paths (LENGTH, NO_KEY, KEY_PHASE).  Reference: _crypto.c:115-204 and
+quic/crypto.py:75-116 through the same C ABI as the quad kernels."""
+
+import numpy as np
+import pytest
+
+from tests.golden_cases import short_header
+from tests.test_gpu_parity import _keys, _random_batch
+
+pytestmark = pytest.mark.gpu
+
+CHUNK = 16
+
+
+@pytest.fixture(scope="module")
+def L():
+    from aioquic_amd import layout
+
+    return layout
+
+
+def _chunks(n, rng):
+    """Chunk sizes 1..16 covering n packets (the lone kernels' launch sizes)."""
+    out, i = [], 0
+    while i < n:
+        k = int(rng.integers(1, CHUNK + 1))
+        out.append(slice(i, min(n, i + k)))
+        i += k
+    return out
+
+
+def _check_round_trip(oracle, L, eng, recs, headers, payloads, pns, slots, rng, flags=0):
+    from aioquic_amd.batch import layout_packets
+
+    n_ok = 0
+    for sl in _chunks(len(headers), rng):
+        h, p, pn, s = headers[sl], payloads[sl], pns[sl], slots[sl]
+        inbuf, desc, size = layout_packets(h, p, pn, s, flags=flags)
+        out_g, res_g = eng.protect_host(desc, inbuf.tobytes(), size)
+        out_o, res_o = oracle.protect_batch(recs, desc, inbuf, size)
+        assert (res_g == res_o).all(), (res_g, res_o)
+        assert np.array_equal(out_g, out_o), sl
+        ud = desc.copy()
+        ud["len"] = res_g["out_len"]
+        if not flags:
+            ud["hdr_len"] = [len(x) - ((x[0] & 3) + 1) for x in h]
+            ud["pn"] = np.asarray(pn, np.uint64) + rng.integers(0, 50, size=len(pn)).astype(np.uint64)
+        wire = out_g.copy()
+        # a tampered packet in about every other chunk
+        t = int(rng.integers(0, 2 * len(h)))
+        if t < len(h) and res_g[t]["status"] == L.S_OK:
+            o = int(desc[t]["out_off"]) + int(rng.integers(len(h[t]), int(res_g[t]["out_len"])))
+            wire[o] ^= 1 << int(rng.integers(0, 8))
+        u_g, r_g = eng.unprotect_host(ud, wire.tobytes(), size)
+        u_o, r_o = oracle.unprotect_batch(recs, ud, wire, size)
+        assert (r_g == r_o).all(), (sl, r_g, r_o)
+        for j in range(len(h)):
+            if r_g[j]["status"] == L.S_OK:
+                o, ln = int(ud[j]["out_off"]), int(r_g[j]["out_len"])
+                assert np.array_equal(u_g[o : o + ln], u_o[o : o + ln]), (sl, j)
+                n_ok += 1
+    return n_ok
+
+
+@pytest.mark.parametrize("suites", [(0,), (1,), (2,), (0, 1, 2)], ids=["aes128", "aes256", "chacha", "mixed"])
+def test_lone_random_packets_vs_oracle(oracle, L, suites):
+    """Short and long headers, pn lengths 1-4, payloads 0..1400 B, several
+    keys: protect and unprotect in launches of 1-16 packets."""
+    from aioquic_amd.batch import PacketEngine
+
+    rng = np.random.default_rng(0x10E + len(suites) + 7 * suites[0])
+    recs = _keys(rng, 6, suites)
+    eng = PacketEngine(6)
+    eng.set_key_records(recs)
+    headers, payloads, pns, slots = _random_batch(rng, 300, 6, recs)
+    # the reference's 4-byte signed-pn quirk packets fail on both sides alike
+    n_ok = _check_round_trip(oracle, L, eng, recs, headers, payloads, pns, slots, rng)
+    assert n_ok > 200  # ~1 in 8 quirk packets, ~1 tampered per 2 chunks
+
+
+@pytest.mark.parametrize("suite", [0, 1, 2])
+def test_lone_aead_only_long_aad(oracle, L, suite):
+    """AEAD.encrypt / decrypt (QPP_F_NO_HP) with associated data up to 1500
+    bytes and data up to the 1500-byte limit: up to 188 GHASH / Poly1305
+    blocks, three per lane, 24 associated-data groups."""
+    from aioquic_amd.batch import PacketEngine
+
+    rng = np.random.default_rng(0xAAD + suite)
+    recs = _keys(rng, 2, (suite,))
+    eng = PacketEngine(2)
+    eng.set_key_records(recs)
+    sizes = [(0, 0), (0, 1), (1, 0), (15, 1), (16, 16), (17, 47), (0, 1484), (1500, 0), (1500, 1484),
+             (1000, 400), (63, 64), (64, 63), (300, 1200), (13, 3)]
+    sizes += [(int(rng.integers(0, 1500)), int(rng.integers(0, 1485))) for _ in range(50)]
+    aads = [rng.bytes(a) for a, _ in sizes]
+    datas = [rng.bytes(b) for _, b in sizes]
+    pns = [int(rng.integers(0, 1 << 62)) for _ in sizes]
+    slots = [i % 2 for i in range(len(sizes))]
+    _check_round_trip(oracle, L, eng, recs, aads, datas, pns, slots, rng, flags=L.F_NO_HP)
+
+
+def test_lone_status_paths(oracle, L):
+    """LENGTH (short data, pn offset 0), NO_KEY (empty and out-of-table
+    slots), KEY_PHASE, DECRYPT, in one launch of 16 packets per suite."""
+    from aioquic_amd.batch import PacketEngine, layout_packets
+
+    rng = np.random.default_rng(0x5747)
+    recs = _keys(rng, 3)
+    eng = PacketEngine(4)
+    eng.set_key_records(recs)
+    n = 16
+    headers = [short_header(rng.bytes(8), i, 2, 0) for i in range(n)]
+    payloads = [rng.bytes(int(rng.integers(4, 1200))) for _ in range(n)]
+    slots = [i % 3 for i in range(n)]
+    inbuf, desc, size = layout_packets(headers, payloads, list(range(n)), slots)
+    out, res = eng.protect_host(desc, inbuf.tobytes(), size)
+    assert (res["status"] == L.S_OK).all()
+    wire = out.copy()
+    o = int(desc[2]["out_off"]) + int(res[2]["out_len"]) - 1
+    wire[o] ^= 4  # the tag's last byte (beyond the HP sample): DECRYPT
+    ud = desc.copy()
+    ud["len"] = res["out_len"]
+    ud["hdr_len"] = 9
+    ud[3]["len"] = 25    # too short for header + tag
+    ud[5]["slot"] = 3    # never installed
+    ud[6]["slot"] = 9    # beyond the table
+    ud[7]["hdr_len"] = 0
+    u, r = eng.unprotect_host(ud, wire.tobytes(), size)
+    uo, ro = oracle.unprotect_batch(recs, ud, wire, size)
+    assert (r == ro).all()
+    assert r[2]["status"] == L.S_DECRYPT and r[3]["status"] == L.S_LENGTH
+    assert r[5]["status"] == L.S_NO_KEY and r[6]["status"] == L.S_NO_KEY
+    assert r[7]["status"] == L.S_LENGTH
+    recs2 = recs.copy()
+    recs2[0]["key_phase"] = 1
+    eng.set_key_records(recs2[:1])
+    u, r = eng.unprotect_host(ud, wire.tobytes(), size)
+    for i in range(0, n, 3):
+        if i not in (3, 6):
+            assert int(r[i]["status"]) == L.S_KEY_PHASE, i
+
+
+def test_lone_matches_quad_kernels_on_device(L):
+    """The same 16-packet device batch through the lone kernels and, in a child
+    process with QPP_LONE=0, through the quad kernels: identical bytes."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); from tests.test_gpu_lone import _device_digest; "
+            "print('digest', _device_digest())" % root)
+    outs = []
+    for lone in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, QPP_LONE=lone),
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+        outs.append([x for x in r.stdout.splitlines() if x.startswith("digest")][-1])
+    assert outs[0] == outs[1]
+
+
+def _device_digest():
+    import hashlib
+
+    import torch
+
+    from aioquic_amd import bench_data
+    from aioquic_amd.batch import PacketEngine
+
+    h = hashlib.sha256()
+    for suite in (0, 1, 2):
+        w = bench_data.make_workload(16, suite=suite, n_keys=2, seed=0x1E + suite)
+        eng = PacketEngine(w.n_keys)
+        eng.set_key_records(w.keys)
+        dev = torch.device("cuda")
+        d_in = torch.from_numpy(w.plain).to(dev)
+        d_desc = torch.from_numpy(w.desc.view(np.uint8)).to(dev)
+        d_wire = torch.zeros(w.wire_size, dtype=torch.uint8, device=dev)
+        d_res = torch.zeros(16 * 16, dtype=torch.uint8, device=dev)
+        eng.protect(d_desc, 16, d_in, d_wire, d_res)
+        d_udesc = torch.from_numpy(w.udesc.view(np.uint8)).to(dev)
+        d_back = torch.zeros(w.plain_size, dtype=torch.uint8, device=dev)
+        d_res2 = torch.zeros(16 * 16, dtype=torch.uint8, device=dev)
+        eng.unprotect(d_udesc, 16, d_wire, d_back, d_res2)
+        torch.cuda.synchronize()
+        for t in (d_wire, d_res, d_back, d_res2):
+            h.update(t.cpu().numpy().tobytes())
+        assert np.array_equal(d_back.cpu().numpy(), w.plain)
+    return h.hexdigest()
+
+
+def test_lone_in_place(oracle, L):
+    """out buffer == in buffer for a 16-packet device launch (the builder
+    encrypts in place, packet_builder.py:341-350), then decrypt in place."""
+    import torch
+
+    from aioquic_amd.batch import PacketEngine, layout_packets
+
+    rng = np.random.default_rng(0x19)
+    recs = _keys(rng, 3)
+    eng = PacketEngine(3)
+    eng.set_key_records(recs)
+    n = 16
+    headers = [short_header(rng.bytes(8), i, 1 + i % 4, 0) for i in range(n)]
+    payloads = [rng.bytes(int(rng.integers(4, 1400))) for _ in range(n)]
+    inbuf, desc, size = layout_packets(headers, payloads, list(range(n)), [i % 3 for i in range(n)])
+    exp, _ = oracle.protect_batch(recs, desc, inbuf, size)
+    buf = torch.from_numpy(inbuf.copy()).cuda()
+    d = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
+    res = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    eng.protect(d, n, buf, buf, res)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    for i in range(n):
+        o, ln = int(desc[i]["out_off"]), len(headers[i]) + len(payloads[i]) + 16
+        assert np.array_equal(got[o : o + ln], exp[o : o + ln]), i
+    ud = desc.copy()
+    ud["len"] = [len(h) + len(p) + 16 for h, p in zip(headers, payloads)]
+    ud["hdr_len"] = [len(h) - ((h[0] & 3) + 1) for h in headers]
+    eng.unprotect(torch.from_numpy(ud.view(np.uint8).copy()).cuda(), n, buf, buf, res)
+    torch.cuda.synchronize()
+    back = buf.cpu().numpy()
+    r = res.cpu().numpy().view(L.RESULT)
+    assert (r["status"] == L.S_OK).all()
+    for i in range(n):
+        o = int(desc[i]["out_off"])
+        assert back[o : o + len(headers[i]) + len(payloads[i])].tobytes() == headers[i] + payloads[i], i
