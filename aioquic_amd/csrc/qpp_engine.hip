@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "qpp_chacha.h"
+#include "qpp_gf128.h"
 #include "qpp_device.h"
 #include "qpp_hkdf.h"
 #include "qpp_internal.h"
@@ -1684,7 +1685,17 @@ __device__ __forceinline__ void lone_protect_hp(Pkt &P, const KeySlot *ks, uint8
     }
 }
 
+__device__ __forceinline__ u32x4 gf_mul(u32x4 x, u32x4 y)
+{
+    const gf::Blk z = gf::mul(gf::Blk{{x.x, x.y, x.z, x.w}}, gf::Blk{{y.x, y.y, y.z, y.w}});
+    return u32x4{z.w[0], z.w[1], z.w[2], z.w[3]};
+}
+
 // One AES-GCM packet per wave (SP 800-38D; _crypto.c:157-204 / :115-155).
+// Lane l takes sequence positions l and l + 64 (and l + 128 beyond 128
+// blocks: long associated data): every load is issued before the first
+// use, both counter blocks run as one aes_ctr2 chain, and the two GHASH
+// terms are independent table-free multiplies (qpp_gf128.h).
 template <int SUITE, bool ENC>
 __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict__ slots,
                                                       const uint8_t *__restrict__ gtab, uint32_t cap,
@@ -1697,22 +1708,19 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
     __shared__ __attribute__((aligned(16))) uint8_t scr[kLoneWG / 64][48];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
+    const bool live = p < n;
+    // the descriptor is requested before the AES image is built
+    qpp_desc d = {0, 0, 0, 0, 0, 0, kNoSlot, 0};
+    if (live) d = desc[p];
     load_te<kLoneWG>(te);
     __syncthreads();
-    if (p >= n) return;
-    const qpp_desc d = desc[p];
-    if (!lone_slot<SUITE>(d, slots, cap, res, p)) return;
+    if (!live || !lone_slot<SUITE>(d, slots, cap, res, p)) return;
     const KeySlot *ks = slots + d.slot;
     const uint32_t lane = lane_fresh();
     const LdsTe T{te, (lane & 31) * 4};
     const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
     Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
     if (P.status == QPP_S_OK) {
-        uint32_t rk[4 * (kNR + 1)];
-#pragma unroll
-        for (int i = 0; i < 4 * (kNR + 1); ++i)
-            rk[i] = __builtin_amdgcn_readfirstlane((i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
-        const CtrCache cc = ctr_cache(P.nonce, rk, T);
         const int hlen = P.hlen, clen = P.clen;
         const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, m = n_a + n_c + 1;
         const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
@@ -1720,31 +1728,51 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         uint8_t *dst = P.dst;
         const uint8_t *hpw = gtab + (size_t)d.slot * kGhashTabBytes + kGhPowOff;
         const bool masked = !ENC && P.hp;
-        // sequence position pos = lane + 64 k: AAD block, CT block or the
-        // lengths block; its GHASH term X_pos H^(m - pos)
-        u32x4 y = zero4(), ej0 = zero4();
-        for (int k = 0; k < 3; ++k) {
-            const int pos = (int)lane + 64 * k;
-            if (pos >= m) break;
-            u32x4 x;
+        // a position's input block (AAD or CT; zero otherwise), its power of H
+        auto input = [&](int pos) -> u32x4 {
+            if (pos < n_a) return ld_win(src + 16 * pos, min(16, hlen - 16 * pos), src, src + rlen);
+            const int i = pos - n_a;
+            if (i < n_c) return ld_win(src + hlen + 16 * i, min(16, clen - 16 * i), src, src + rlen);
+            return zero4();
+        };
+        auto power = [&](int pos) -> u32x4 { return pos < m ? ld16(hpw + 16 * (m - 1 - pos)) : zero4(); };
+        const int pos0 = (int)lane, pos1 = (int)lane + 64;
+        const u32x4 in0 = input(pos0), in1 = input(pos1), h0 = power(pos0), h1 = power(pos1);
+        uint32_t rk[4 * (kNR + 1)];
+#pragma unroll
+        for (int i = 0; i < 4 * (kNR + 1); ++i)
+            rk[i] = __builtin_amdgcn_readfirstlane((i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
+        const CtrCache cc = ctr_cache(P.nonce, rk, T);
+        // CT block i: counter i + 2; the lengths position: J0 (counter 1)
+        auto ctr = [&](int pos) -> uint32_t {
+            return (pos >= n_a && pos < n_a + n_c) ? (uint32_t)(pos - n_a + 2) : 1u;
+        };
+        // a position's output and GHASH input given its keystream
+        u32x4 ej0 = zero4();
+        auto out = [&](int pos, u32x4 in, u32x4 ksb) -> u32x4 {
+            u32x4 x = zero4();
             if (pos < n_a) {
-                const int nb = min(16, hlen - 16 * pos);
-                x = ld_win(src + 16 * pos, nb, src, src + rlen);
+                x = in;
                 if (masked) x ^= hp_pattern(16 * pos, P.mask, P.fbm, P.pn_off, P.pn_len);
-                if (!ENC || !P.hp) st_part(dst + 16 * pos, x, nb);
+                if (!ENC || !P.hp) st_part(dst + 16 * pos, x, min(16, hlen - 16 * pos));
             } else if (pos < n_a + n_c) {
                 const int i = pos - n_a, nb = min(16, clen - 16 * i);
-                const u32x4 in = ld_win(src + hlen + 16 * i, nb, src, src + rlen);
-                const u32x4 o = in ^ aes_ctr<kNR>(cc, (uint32_t)(i + 2), rk, T);
+                const u32x4 o = in ^ ksb;
                 st_part(dst + hlen + 16 * i, o, nb);
                 x = keep_bytes(ENC ? o : in, nb);
                 if (ENC && P.hp && i < 2) *(u32x4 *)(scr[wv] + 16 * i) = x;
-            } else {
+            } else if (pos == m - 1) {
                 x = u32x4{0u, bswap((uint32_t)hlen * 8u), 0u, bswap((uint32_t)clen * 8u)};
-                ej0 = aes_ctr<kNR>(cc, 1u, rk, T);
+                ej0 = ksb;
             }
-            y ^= gf128_mul_slow(x, ld16(hpw + 16 * (m - 1 - pos)));
-        }
+            return x;
+        };
+        u32x4 ks0, ks1;
+        aes_ctr2<kNR>(cc, ctr(pos0), ctr(pos1), rk, T, ks0, ks1);
+        const u32x4 x0 = out(pos0, in0, ks0), x1 = out(pos1, in1, ks1);
+        u32x4 y = gf_mul(x0, h0) ^ gf_mul(x1, h1);
+        for (int pos = (int)lane + 128; pos < m; pos += 64)  // > 128 blocks
+            y ^= gf_mul(out(pos, input(pos), aes_ctr<kNR>(cc, ctr(pos), rk, T)), power(pos));
         const u32x4 tag = u32x4{wave_xor_u32(y.x), wave_xor_u32(y.y), wave_xor_u32(y.z), wave_xor_u32(y.w)} ^
                           readlane4(ej0, (m - 1) & 63);
         if (ENC) {
@@ -1754,10 +1782,8 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
             const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
             if ((diff.x | diff.y | diff.z | diff.w) != 0) {
                 P.status = QPP_S_DECRYPT;
-                for (int k = 0; k < 3; ++k) {
-                    const int i = (int)lane + 64 * k - n_a;
-                    if (i >= 0 && i < n_c) st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
-                }
+                for (int i = (int)lane - n_a; i < n_c; i += 64)
+                    if (i >= 0) st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
             }
         }
     }
@@ -1768,7 +1794,9 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
 // one-time key block; lane u = 1..24: chunk u - 1 (4 CT blocks); lane 32 + g:
 // AAD blocks 4g..4g+3; lane 63: the lengths block.  Each lane folds its
 // blocks by Horner in r and scales the result by r^e, e = m - (position of
-// its last block); the 26-bit limbs of <= 49 terms sum without carries.
+// its last block); r^e by square-and-multiply beside the Horner chain; the
+// 26-bit limbs of <= 49 terms sum without carries.  The lane's input blocks
+// are requested before its ChaCha20 block.
 template <bool ENC>
 __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restrict__ slots, uint32_t cap,
                                                          const qpp_desc *__restrict__ desc, uint32_t n,
@@ -1794,6 +1822,31 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
         const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
         const uint8_t *src = P.src;
         uint8_t *dst = P.dst;
+        // this lane's blocks: first sequence position q, count cnt
+        const bool is_ct = lane >= 1 && (int)lane <= chunks;
+        const int g = (int)lane - 32, c0 = 4 * ((int)lane - 1);
+        int q = 0, cnt = 0;
+        if (is_ct) {
+            q = n_a + c0;
+            cnt = min(4, n_c - c0);
+        } else if (g >= 0 && 4 * g < n_a) {
+            q = 4 * g;
+            cnt = min(4, n_a - 4 * g);
+        } else if (lane == 63) {
+            q = m - 1;
+            cnt = 1;
+        }
+        // the blocks' inputs first
+        u32x4 in[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            in[b] = zero4();
+            if (b < cnt && lane != 63) {
+                const int j = is_ct ? hlen + 16 * (c0 + b) : 16 * (4 * g + b);
+                const int nb = is_ct ? min(16, clen - 16 * (c0 + b)) : min(16, hlen - 16 * (4 * g + b));
+                in[b] = ld_win(src + j, nb, src, src + rlen);
+            }
+        }
         uint32_t key[8];
 #pragma unroll
         for (int w = 0; w < 8; ++w) key[w] = __builtin_amdgcn_readfirstlane(ks->rk[w]);
@@ -1803,50 +1856,42 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
 #pragma unroll
         for (int w = 0; w < 8; ++w) kw[w] = (uint32_t)__builtin_amdgcn_readlane((int)blk[w], 0);
         const P130 r = p130_r(kw[0], kw[1], kw[2], kw[3]);
-        // this lane's blocks: first sequence position q, count nb
-        const bool is_ct = lane >= 1 && (int)lane <= chunks;
-        const int g = (int)lane - 32;
-        int q = 0, cnt = 0;
-        if (is_ct) {
-            q = n_a + 4 * ((int)lane - 1);
-            cnt = min(4, n_c - 4 * ((int)lane - 1));
-        } else if (g >= 0 && 4 * g < n_a) {
-            q = 4 * g;
-            cnt = min(4, n_a - 4 * g);
-        } else if (lane == 63) {
-            q = m - 1;
-            cnt = 1;
-        }
+        // r^e, e = m - (q + cnt - 1), beside the Horner chain
+        const int e = cnt > 0 ? m - (q + cnt - 1) : 0;
+        P130 rp = r, re = p130_zero();
+        re.v[0] = 1u;
         const bool masked = !ENC && P.hp;
         P130 w = p130_zero();
-        for (int b = 0; b < cnt; ++b) {
-            u32x4 x;
-            if (is_ct) {
-                const int i = 4 * ((int)lane - 1) + b, nb = min(16, clen - 16 * i);
-                const u32x4 in = ld_win(src + hlen + 16 * i, nb, src, src + rlen);
-                const u32x4 o = in ^ u32x4{blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3]};
-                st_part(dst + hlen + 16 * i, o, nb);
-                x = keep_bytes(ENC ? o : in, nb);
-                if (ENC && P.hp && i < 2) *(u32x4 *)(scr[wv] + 16 * i) = x;
-            } else if (lane == 63) {
-                x = u32x4{(uint32_t)hlen, 0u, (uint32_t)clen, 0u};
-            } else {
-                const int j = 4 * g + b, nb = min(16, hlen - 16 * j);
-                x = ld_win(src + 16 * j, nb, src, src + rlen);
-                if (masked) x ^= hp_pattern(16 * j, P.mask, P.fbm, P.pn_off, P.pn_len);
-                if (!ENC || !P.hp) st_part(dst + 16 * j, x, nb);
-            }
-            w = p130_add(b == 0 ? w : p130_mul(w, r), p130_block(x));
-        }
-        // w r^e, e = m - (q + cnt - 1) (a lane without blocks holds 0)
-        const int e = cnt > 0 ? m - (q + cnt - 1) : 0;
-        P130 rp = r, one = p130_zero();
-        one.v[0] = 1u;
 #pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            w = p130_mul(w, ((e >> bit) & 1) ? rp : one);
-            if (bit < 7) rp = p130_mul(rp, rp);
+        for (int b = 0; b < 4; ++b) {
+            u32x4 x = zero4();
+            if (b < cnt) {
+                if (is_ct) {
+                    const int i = c0 + b, nb = min(16, clen - 16 * i);
+                    const u32x4 o = in[b] ^ u32x4{blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3]};
+                    st_part(dst + hlen + 16 * i, o, nb);
+                    x = keep_bytes(ENC ? o : in[b], nb);
+                    if (ENC && P.hp && i < 2) *(u32x4 *)(scr[wv] + 16 * i) = x;
+                } else if (lane == 63) {
+                    x = u32x4{(uint32_t)hlen, 0u, (uint32_t)clen, 0u};
+                } else {
+                    const int j = 4 * g + b;
+                    x = in[b];
+                    if (masked) x ^= hp_pattern(16 * j, P.mask, P.fbm, P.pn_off, P.pn_len);
+                    if (!ENC || !P.hp) st_part(dst + 16 * j, x, min(16, hlen - 16 * j));
+                }
+            }
+            // Horner: w = w r + M_b over the lane's blocks (one more block
+            // than it has only multiplies zero)
+            const P130 mb = p130_block(x);
+            if (b < cnt) w = p130_add(b == 0 ? w : p130_mul(w, r), mb);
+            // two steps of the power chain per block step (8 bits of e)
+            re = p130_mul(re, ((e >> (2 * b)) & 1) ? rp : P130{{1u, 0u, 0u, 0u, 0u}});
+            rp = p130_mul(rp, rp);
+            re = p130_mul(re, ((e >> (2 * b + 1)) & 1) ? rp : P130{{1u, 0u, 0u, 0u, 0u}});
+            if (b < 3) rp = p130_mul(rp, rp);
         }
+        w = p130_mul(w, re);
         P130 sum;
 #pragma unroll
         for (int l = 0; l < 5; ++l) sum.v[l] = wave_sum_u32(w.v[l]);
@@ -1860,7 +1905,7 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
                 P.status = QPP_S_DECRYPT;
                 if (is_ct)
                     for (int b = 0; b < cnt; ++b) {
-                        const int i = 4 * ((int)lane - 1) + b;
+                        const int i = c0 + b;
                         st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
                     }
             }
