@@ -1924,15 +1924,21 @@ __global__ __launch_bounds__(kMaskWG) void k_hp_mask(const KeySlot *__restrict__
                                                      uint32_t n, uint8_t *__restrict__ masks)
 {
     __shared__ __attribute__((aligned(16))) uint8_t te[kTeBytes];
+    const uint32_t i = blockIdx.x * kMaskWG + threadIdx.x;
+    // the slot and sample are requested before the AES image is built (a
+    // one-mask call is latency: HeaderProtection.apply / remove)
+    uint32_t s = kNoSlot;
+    u32x4 smp = {0, 0, 0, 0};
+    if (i < n) {
+        s = sidx[i];
+        smp = ld16(samples + 16 * (size_t)i);
+    }
     load_te<kMaskWG>(te);
     __syncthreads();
     const LdsTe T{te, (uint32_t)(threadIdx.x & 31) * 4};
-    const uint32_t i = blockIdx.x * kMaskWG + threadIdx.x;
     if (i >= n) return;
-    const uint32_t s = sidx[i];
     u32x4 m = {0, 0, 0, 0};
-    if (s < cap && slots[s].suite <= QPP_CHACHA20_POLY1305)
-        m = hp_mask_any(slots + s, slots[s].suite, ld16(samples + 16 * (size_t)i), T);
+    if (s < cap && slots[s].suite <= QPP_CHACHA20_POLY1305) m = hp_mask_any(slots + s, slots[s].suite, smp, T);
     st16(masks + 16 * (size_t)i, m);
 }
 
@@ -2156,6 +2162,7 @@ struct qpp_session {
     size_t max_bytes;
     uint32_t max_packets;
     uint8_t *h_in, *h_out, *h_misc;  // pinned
+    uint8_t *hd_in, *hd_out, *hd_misc;  // their device views (zero-copy small calls)
     uint8_t *d_in, *d_out, *d_misc;
     size_t misc_bytes;
     qpp_plan *plan;                  // bucketing of batches of >= kSessionPlanMin packets
@@ -2369,6 +2376,20 @@ static bool lone_choice()
     return b;
 }
 
+// Small host calls on the lone-packet kernels (and small header-protection
+// mask calls) read and write the session's pinned staging from the kernel
+// instead of through two copy-engine blits (~3.8 us each plus their
+// scheduling, profiles/r4j_lone_latency); QPP_ZERO_COPY=0 keeps the copies
+// (a study and test switch, read once per process).
+static bool zero_copy_choice()
+{
+    static const bool b = [] {
+        const char *v = getenv("QPP_ZERO_COPY");
+        return !(v && v[0] == '0');
+    }();
+    return b;
+}
+
 static uint32_t cu_count()
 {
     static int cus[64];
@@ -2562,6 +2583,7 @@ static void session_free_buffers(qpp_session *s)
     if (s->d_out) (void)hipFree(s->d_out);
     if (s->d_misc) (void)hipFree(s->d_misc);
     s->h_in = s->h_out = s->h_misc = s->d_in = s->d_out = s->d_misc = NULL;
+    s->hd_in = s->hd_out = s->hd_misc = NULL;
 }
 
 static size_t misc_bytes_for(uint32_t max_packets)
@@ -2585,7 +2607,10 @@ static int session_reserve(qpp_session *s, size_t bytes, uint32_t packets)
         hipHostMalloc(&s->h_out, nb, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&s->h_misc, s->misc_bytes, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&s->d_in, nb) != hipSuccess || hipMalloc(&s->d_out, nb) != hipSuccess ||
-        hipMalloc(&s->d_misc, s->misc_bytes) != hipSuccess) {
+        hipMalloc(&s->d_misc, s->misc_bytes) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&s->hd_in, s->h_in, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&s->hd_out, s->h_out, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&s->hd_misc, s->h_misc, 0) != hipSuccess) {
         (void)hipGetLastError();
         session_free_buffers(s);
         s->max_bytes = 0;
@@ -2851,6 +2876,21 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
         reject_out_of_bounds(enc, (qpp_desc *)h, n, in_len, out_len);
         if (in_len) memcpy(h + sd, in, in_len);
         memset(h + sd + si, 0, out_len);  // bytes the kernel does not write come back as zeros
+        if (n <= kLoneMax && lone_choice() && zero_copy_choice()) {
+            // one wave per packet: descriptors and input by one copy, the
+            // output and results written by the kernel straight into the
+            // pinned staging (PCIe writes post; reads there would put a bus
+            // round trip on each of the kernel's dependent loads)
+            HIPCHK(hipMemcpyAsync(d, h, sd + si, hipMemcpyHostToDevice, s->stream));
+            uint8_t *dh = s->hd_in;
+            rc = launch_packets(enc, kt, (const qpp_desc *)d, n, d + sd, dh + sd + si,
+                                (qpp_result *)(dh + sd + si + so), s->stream);
+            if (rc != QPP_OK) return rc;
+            HIPCHK(hipStreamSynchronize(s->stream));
+            if (out_len) memcpy(out, h + sd + si, out_len);
+            memcpy(res, h + sd + si + so, (size_t)n * sizeof(qpp_result));
+            return QPP_OK;
+        }
         HIPCHK(hipMemcpyAsync(d, h, sd + si + out_len, hipMemcpyHostToDevice, s->stream));
         rc = launch_packets(enc, kt, (const qpp_desc *)d, n, d + sd, d + sd + si,
                             (qpp_result *)(d + sd + si + so), s->stream);
@@ -2918,6 +2958,13 @@ int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *sl
     uint32_t *hidx = (uint32_t *)s->h_misc;
     memcpy(hidx, slots, (size_t)n * 4);
     memcpy(hs, samples, (size_t)n * 16);
+    if (n <= kSmallPackets && zero_copy_choice()) {
+        rc = qpp_hp_mask(kt, (const uint32_t *)s->hd_misc, s->hd_in, n, s->hd_out, s->stream);
+        if (rc != QPP_OK) return rc;
+        HIPCHK(hipStreamSynchronize(s->stream));
+        memcpy(masks, hm, (size_t)n * 16);
+        return QPP_OK;
+    }
     HIPCHK(hipMemcpyAsync(s->d_misc, hidx, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
     HIPCHK(hipMemcpyAsync(s->d_in, hs, (size_t)n * 16, hipMemcpyHostToDevice, s->stream));
     rc = qpp_hp_mask(kt, (const uint32_t *)s->d_misc, s->d_in, n, s->d_out, s->stream);

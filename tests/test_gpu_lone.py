@@ -230,3 +230,34 @@ def test_lone_in_place(oracle, L):
     for i in range(n):
         o = int(desc[i]["out_off"])
         assert back[o : o + len(headers[i]) + len(payloads[i])].tobytes() == headers[i] + payloads[i], i
+
+
+def test_lone_through_staging_copies():
+    """The same small host calls with QPP_ZERO_COPY=0 (the session's staged
+    copies instead of the kernel reading and writing pinned memory), in a
+    child process, against the oracle."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); from tests.test_gpu_lone import _child_check; _child_check()" % root)
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, QPP_ZERO_COPY="0"),
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "lone child ok" in r.stdout
+
+
+def _child_check():
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import PacketEngine
+    from oracle import oracle as orc
+
+    orc.lib()
+    rng = np.random.default_rng(0xC0B1)
+    recs = _keys(rng, 6)
+    eng = PacketEngine(6)
+    eng.set_key_records(recs)
+    headers, payloads, pns, slots = _random_batch(rng, 120, 6, recs)
+    _check_round_trip(orc, L, eng, recs, headers, payloads, pns, slots, rng)
+    print("lone child ok")
