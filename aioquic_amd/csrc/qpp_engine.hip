@@ -1610,8 +1610,10 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
 //   sum_i X_i K^(m - i)   over the m blocks [AAD | CT | lengths],
 // each lane multiplying its blocks by their own power of K (H^e from the
 // slot's power table, r^e by square-and-multiply), and one wave reduction.
+// Launches stay latency-bound up to a few thousand packets (one workgroup
+// of 16 packets per CU), so unplanned launches up to lone_max take these
+// kernels; past that the quad kernels' ~7x fewer instructions per packet win.
 constexpr int kLoneWG = 1024;      // 16 packets per workgroup, one AES image
-constexpr uint32_t kLoneMax = 16;  // unplanned launches of at most this many packets
 
 __device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v)
 {
@@ -2364,7 +2366,7 @@ static int gcm_bpl_choice()
     return b;
 }
 
-// Lone-packet kernels for small unplanned launches (k_lone_gcm /
+// Lone-packet kernels for unplanned launches up to lone_max (k_lone_gcm /
 // k_lone_chacha); QPP_LONE=0 sends them through the quad kernels instead
 // (a study and test switch, read once per process).
 static bool lone_choice()
@@ -2374,6 +2376,24 @@ static bool lone_choice()
         return !(v && v[0] == '0');
     }();
     return b;
+}
+
+// The largest unplanned launch of a suite that takes the lone kernels: where
+// one wave per packet stops beating the quad kernels on the same box
+// (profiles/r4o_lone_crossover.txt, protect: AES-GCM 28.9 against 57.9 us at
+// 4096 packets, 49 against 59 at 8192, 88 against 63 at 16384; ChaCha20
+// 12.9 against 28.9 at 2 packets, then within +-1-3 us of the quad kernel up
+// to 4096 and 47.5 against 30.6 at 8192, so past the host path's small
+// calls the quad kernel's fewer instructions keep it).  QPP_LONE_MAX
+// overrides both (a study switch for tools/lone_sizes.py).
+static uint32_t lone_max(int suite)
+{
+    static const long env = [] {
+        const char *v = getenv("QPP_LONE_MAX");
+        return v ? atol(v) : -1L;
+    }();
+    if (env >= 0) return (uint32_t)(env > (1 << 20) ? (1 << 20) : env);
+    return suite == QPP_CHACHA20_POLY1305 ? 64u : 8192u;
 }
 
 // Small host calls on the lone-packet kernels (and small header-protection
@@ -2445,34 +2465,11 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     // planned: each suite's launch covers at most every wave item of the batch
     const uint32_t *d_items = plan ? plan->d_items : nullptr, *d_irange = plan ? plan->d_irange : nullptr;
     const uint32_t waves = plan ? qpp_internal_plan_max_items(n, kt->cap) : (n + 15) / 16;
-    if (!plan && n <= kLoneMax && lone_choice()) {
-        // a few packets (the object API): one wave per packet
-        const dim3 grid((n + kLoneWG / 64 - 1) / (kLoneWG / 64)), block(kLoneWG);
-#define QPP_LAUNCH_LONE_GCM(SUITE)                                                                 \
-    if (mask & (1u << SUITE)) {                                                                    \
-        if (enc)                                                                                   \
-            hipLaunchKernelGGL((k_lone_gcm<SUITE, true>), grid, block, 0, s, kt->d_slots, kt->d_gtab, \
-                               kt->cap, d_desc, n, d_in, d_out, d_res);                            \
-        else                                                                                       \
-            hipLaunchKernelGGL((k_lone_gcm<SUITE, false>), grid, block, 0, s, kt->d_slots,           \
-                               kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);                \
-        HIPCHK(hipGetLastError());                                                                 \
-    }
-        QPP_LAUNCH_LONE_GCM(QPP_AES_128_GCM)
-        QPP_LAUNCH_LONE_GCM(QPP_AES_256_GCM)
-#undef QPP_LAUNCH_LONE_GCM
-        if (mask & (1u << QPP_CHACHA20_POLY1305)) {
-            if (enc)
-                hipLaunchKernelGGL((k_lone_chacha<true>), grid, block, 0, s, kt->d_slots, kt->cap, d_desc, n,
-                                   d_in, d_out, d_res);
-            else
-                hipLaunchKernelGGL((k_lone_chacha<false>), grid, block, 0, s, kt->d_slots, kt->cap, d_desc, n,
-                                   d_in, d_out, d_res);
-            HIPCHK(hipGetLastError());
-        }
-        return QPP_OK;
-    }
     const int bpl_gcm = gcm_bpl_choice();
+    // up to a few thousand packets (the object API's one, small flushes):
+    // one wave per packet (k_lone_*), see lone_max
+    const bool lone = !plan && lone_choice();
+    const dim3 lgrid((n + kLoneWG / 64 - 1) / (kLoneWG / 64)), lblock(kLoneWG);
 #define QPP_LAUNCH_GCM_W(SUITE, BPLV, WGV)                                                     \
     do {                                                                                       \
         const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
@@ -2492,13 +2489,31 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     } while (0)
 #define QPP_LAUNCH_GCM(SUITE)                                                                  \
     if (mask & (1u << SUITE)) {                                                                \
-        if (bpl_gcm == 1) QPP_LAUNCH_GCM_B(SUITE, 1);                                           \
-        else QPP_LAUNCH_GCM_B(SUITE, 2);                                                        \
+        if (lone && n <= lone_max(SUITE)) {                                                    \
+            if (enc)                                                                           \
+                hipLaunchKernelGGL((k_lone_gcm<SUITE, true>), lgrid, lblock, 0, s, kt->d_slots, \
+                                   kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);        \
+            else                                                                               \
+                hipLaunchKernelGGL((k_lone_gcm<SUITE, false>), lgrid, lblock, 0, s, kt->d_slots, \
+                                   kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);        \
+        } else if (bpl_gcm == 1) {                                                             \
+            QPP_LAUNCH_GCM_B(SUITE, 1);                                                         \
+        } else {                                                                               \
+            QPP_LAUNCH_GCM_B(SUITE, 2);                                                         \
+        }                                                                                      \
         HIPCHK(hipGetLastError());                                                             \
     }
     QPP_LAUNCH_GCM(QPP_AES_128_GCM)
     QPP_LAUNCH_GCM(QPP_AES_256_GCM)
-    if (mask & (1u << QPP_CHACHA20_POLY1305)) {
+    if ((mask & (1u << QPP_CHACHA20_POLY1305)) && lone && n <= lone_max(QPP_CHACHA20_POLY1305)) {
+        if (enc)
+            hipLaunchKernelGGL((k_lone_chacha<true>), lgrid, lblock, 0, s, kt->d_slots, kt->cap, d_desc, n, d_in,
+                               d_out, d_res);
+        else
+            hipLaunchKernelGGL((k_lone_chacha<false>), lgrid, lblock, 0, s, kt->d_slots, kt->cap, d_desc, n, d_in,
+                               d_out, d_res);
+        HIPCHK(hipGetLastError());
+    } else if (mask & (1u << QPP_CHACHA20_POLY1305)) {
         const dim3 grid((waves + kChachaWG / 64 - 1) / (kChachaWG / 64)), block(kChachaWG);
         if (enc)
             hipLaunchKernelGGL((k_chacha<true, kChachaWG>), grid, block, 0, s, kt->d_slots, kt->cap,
@@ -2876,7 +2891,8 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
         reject_out_of_bounds(enc, (qpp_desc *)h, n, in_len, out_len);
         if (in_len) memcpy(h + sd, in, in_len);
         memset(h + sd + si, 0, out_len);  // bytes the kernel does not write come back as zeros
-        if (n <= kLoneMax && lone_choice() && zero_copy_choice()) {
+        if (n <= std::min(lone_max(QPP_AES_128_GCM), lone_max(QPP_CHACHA20_POLY1305)) && lone_choice() &&
+            zero_copy_choice()) {
             // one wave per packet: descriptors and input by one copy, the
             // output and results written by the kernel straight into the
             // pinned staging (PCIe writes post; reads there would put a bus

@@ -1,6 +1,6 @@
 """Lone-packet kernels (k_lone_gcm / k_lone_chacha: one wave per packet, for
-unplanned launches of at most 16 packets -- the object API's one packet per
-call) against the C oracle, chunk by chunk: every suite, short and long
+unplanned launches of up to a few thousand packets -- the object API's one
+packet per call, small flushes) against the C oracle, chunk by chunk: every suite, short and long
 headers, AEAD-only with associated data up to 1500 bytes, payloads from 0 to
 the 1500-byte limit, tiny inputs, in-place operation, tampered tags and the
 status paths (LENGTH, NO_KEY, KEY_PHASE).  Reference: _crypto.c:115-204 and
@@ -261,3 +261,38 @@ def _child_check():
     headers, payloads, pns, slots = _random_batch(rng, 120, 6, recs)
     _check_round_trip(orc, L, eng, recs, headers, payloads, pns, slots, rng)
     print("lone child ok")
+
+
+def test_quad_kernels_at_small_sizes():
+    """With the lone kernels taking unplanned launches of up to a few thousand
+    packets, the quad kernels' small-launch paths (golden vectors, in place,
+    tampering) run in a child process with QPP_LONE=0, against the oracle."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); from tests.test_gpu_lone import _quad_child; _quad_child()" % root)
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, QPP_LONE="0"),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "quad child ok" in r.stdout
+
+
+def _quad_child():
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import PacketEngine
+    from oracle import oracle as orc
+    from tests import test_gpu_parity as T
+
+    orc.lib()
+    T.test_golden_vectors_batch(orc, L, PacketEngine)
+    T.test_in_place(orc, L, PacketEngine)
+    T.test_tamper_and_edge_status(orc, L, PacketEngine)
+    rng = np.random.default_rng(0x0AD)
+    recs = _keys(rng, 6)
+    eng = PacketEngine(6)
+    eng.set_key_records(recs)
+    headers, payloads, pns, slots = _random_batch(rng, 120, 6, recs)
+    _check_round_trip(orc, L, eng, recs, headers, payloads, pns, slots, rng)
+    print("quad child ok")
