@@ -19,10 +19,10 @@ module in its place.  The design underneath differs:
 
 from __future__ import annotations
 
+import struct
 from dataclasses import dataclass
 from typing import Callable, Dict, Optional, Tuple
 
-import numpy as np
 
 from . import layout as L
 from ._crypto import AEAD, CryptoError, HeaderProtection, KeyTable, protect_host, unprotect_host
@@ -94,11 +94,28 @@ def _status_error(status: int) -> Exception:
     return CryptoError("Invalid payload length")
 
 
+# one qpp_desc / qpp_result (layout.DESC / layout.RESULT) by struct: the
+# per-packet calls build and read one record each, where numpy's structured
+# arrays cost microseconds per call
+_DESC = struct.Struct("<QQIHHQII")
+_RESULT = struct.Struct("<QHHI")
+assert _DESC.size == L.DESC.itemsize and _RESULT.size == L.RESULT.itemsize
+
+
 def _one_desc(length: int, hdr_len: int, pn: int, slot: int) -> bytes:
-    rec = np.zeros(1, dtype=L.DESC)
-    rec[0]["len"], rec[0]["hdr_len"], rec[0]["slot"] = length, hdr_len, slot
-    rec[0]["pn"] = pn & 0xFFFFFFFFFFFFFFFF
-    return rec.tobytes()
+    return _DESC.pack(0, 0, length, hdr_len, 0, pn & 0xFFFFFFFFFFFFFFFF, slot, 0)
+
+
+class _Result:
+    """One qpp_result, read from the library's bytes."""
+
+    __slots__ = ("pn", "status", "hdr_len", "out_len")
+
+    def __init__(self, raw: bytes) -> None:
+        self.pn, self.status, self.hdr_len, self.out_len = _RESULT.unpack_from(raw)
+
+    def __getitem__(self, field: str) -> int:
+        return getattr(self, field)
 
 
 class _PhaseSlots:
@@ -126,7 +143,7 @@ class _PhaseSlots:
 def _unprotect_once(table: KeyTable, packet: bytes, offset: int, expected: int, slot: int):
     desc = _one_desc(len(packet), offset, expected, slot)
     out, res = unprotect_host(table, desc, packet, len(packet))
-    return out, np.frombuffer(res, dtype=L.RESULT)[0]
+    return out, _Result(res)
 
 
 class CryptoContext:
@@ -178,7 +195,7 @@ class CryptoContext:
         total = len(plain_header) + len(plain_payload) + L.TAG_LEN
         desc = _one_desc(len(plain_payload), len(plain_header), packet_number, 0)
         out, res = protect_host(dev.table, desc, plain_header + plain_payload, total)
-        status = int(np.frombuffer(res, dtype=L.RESULT)[0]["status"])
+        status = _RESULT.unpack_from(res)[1]
         if status != L.S_OK:
             raise _status_error(status)
         return out

@@ -1615,6 +1615,34 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
 // kernels; past that the quad kernels' ~7x fewer instructions per packet win.
 constexpr int kLoneWG = 1024;      // 16 packets per workgroup, one AES image
 
+// A small host call handed to a lone kernel whole (qpp_session): the kernel
+// copies the call's descriptors and input from the pinned staging (src, its
+// device view) into the device staging (dst) itself, every thread 16 bytes
+// in one bus round trip, instead of a copy-engine blit scheduled between
+// stream operations.  bytes == 0: nothing staged (device-buffer launches).
+// One workgroup (at most 16 packets); the workgroup barrier makes the copy
+// visible to its waves (vector L1 writes through to L2).
+struct LoneStage {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint32_t bytes;  // multiple of 16, <= kLoneStageMax
+};
+constexpr uint32_t kLoneStageMax = 2 * kLoneWG * 16;
+
+__device__ __forceinline__ void lone_stage_load(const LoneStage &st, u32x4 &a, u32x4 &b)
+{
+    const uint32_t o = threadIdx.x * 16u;
+    a = o < st.bytes ? ld16(st.src + o) : zero4();
+    b = o + kLoneWG * 16u < st.bytes ? ld16(st.src + o + kLoneWG * 16u) : zero4();
+}
+
+__device__ __forceinline__ void lone_stage_store(const LoneStage &st, u32x4 a, u32x4 b)
+{
+    const uint32_t o = threadIdx.x * 16u;
+    if (o < st.bytes) st16(st.dst + o, a);
+    if (o + kLoneWG * 16u < st.bytes) st16(st.dst + o + kLoneWG * 16u, b);
+}
+
 __device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v)
 {
     v ^= dpp_mov<kDppQuadSwap1>(v);
@@ -1699,11 +1727,13 @@ __device__ __forceinline__ u32x4 gf_mul(u32x4 x, u32x4 y)
 // use, both counter blocks run as one aes_ctr2 chain, and the two GHASH
 // terms are independent table-free multiplies (qpp_gf128.h).
 template <int SUITE, bool ENC>
+// (desc is not __restrict__: with a staged call it is the copy this kernel
+// writes, so its loads must not move above the staging)
 __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict__ slots,
                                                       const uint8_t *__restrict__ gtab, uint32_t cap,
-                                                      const qpp_desc *__restrict__ desc, uint32_t n,
+                                                      const qpp_desc *desc, uint32_t n,
                                                       const uint8_t *gin, uint8_t *gout,
-                                                      qpp_result *__restrict__ res)
+                                                      qpp_result *__restrict__ res, LoneStage st)
 {
     constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
     __shared__ __attribute__((aligned(16))) uint8_t te[kTeBytes];
@@ -1711,11 +1741,21 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
     const bool live = p < n;
-    // the descriptor is requested before the AES image is built
     qpp_desc d = {0, 0, 0, 0, 0, 0, kNoSlot, 0};
-    if (live) d = desc[p];
-    load_te<kLoneWG>(te);
-    __syncthreads();
+    if (st.bytes) {
+        // the call's bytes in flight beside the AES image build
+        u32x4 a, b;
+        lone_stage_load(st, a, b);
+        load_te<kLoneWG>(te);
+        lone_stage_store(st, a, b);
+        __syncthreads();
+        if (live) d = desc[p];
+    } else {
+        // the descriptor is requested before the AES image is built
+        if (live) d = desc[p];
+        load_te<kLoneWG>(te);
+        __syncthreads();
+    }
     if (!live || !lone_slot<SUITE>(d, slots, cap, res, p)) return;
     const KeySlot *ks = slots + d.slot;
     const uint32_t lane = lane_fresh();
@@ -1801,14 +1841,20 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
 // are requested before its ChaCha20 block.
 template <bool ENC>
 __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restrict__ slots, uint32_t cap,
-                                                         const qpp_desc *__restrict__ desc, uint32_t n,
+                                                         const qpp_desc *desc, uint32_t n,
                                                          const uint8_t *gin, uint8_t *gout,
-                                                         qpp_result *__restrict__ res)
+                                                         qpp_result *__restrict__ res, LoneStage st)
 {
     constexpr int SUITE = QPP_CHACHA20_POLY1305;
     __shared__ __attribute__((aligned(16))) uint8_t scr[kLoneWG / 64][48];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
+    if (st.bytes) {
+        u32x4 a, b;
+        lone_stage_load(st, a, b);
+        lone_stage_store(st, a, b);
+        __syncthreads();
+    }
     if (p >= n) return;
     const qpp_desc d = desc[p];
     if (!lone_slot<SUITE>(d, slots, cap, res, p)) return;
@@ -2410,6 +2456,18 @@ static bool zero_copy_choice()
     return b;
 }
 
+// A small host call of one workgroup's packets staged by the lone kernel
+// itself instead of a copy (QPP_LONE_STAGE=0: the copy; a study and test
+// switch, read once per process).
+static bool lone_stage_choice()
+{
+    static const bool b = [] {
+        const char *v = getenv("QPP_LONE_STAGE");
+        return !(v && v[0] == '0');
+    }();
+    return b;
+}
+
 static uint32_t cu_count()
 {
     static int cus[64];
@@ -2452,7 +2510,7 @@ static bool gcm_two_wg(const qpp_keytab *kt, uint32_t suite, uint32_t items)
 
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                           const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream,
-                          const qpp_plan *plan = nullptr)
+                          const qpp_plan *plan = nullptr, const LoneStage *stage = nullptr)
 {
     if (!kt || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
@@ -2470,6 +2528,7 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     // one wave per packet (k_lone_*), see lone_max
     const bool lone = !plan && lone_choice();
     const dim3 lgrid((n + kLoneWG / 64 - 1) / (kLoneWG / 64)), lblock(kLoneWG);
+    const LoneStage lst = stage ? *stage : LoneStage{nullptr, nullptr, 0u};
 #define QPP_LAUNCH_GCM_W(SUITE, BPLV, WGV)                                                     \
     do {                                                                                       \
         const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
@@ -2492,10 +2551,10 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
         if (lone && n <= lone_max(SUITE)) {                                                    \
             if (enc)                                                                           \
                 hipLaunchKernelGGL((k_lone_gcm<SUITE, true>), lgrid, lblock, 0, s, kt->d_slots, \
-                                   kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);        \
+                                   kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, lst);   \
             else                                                                               \
                 hipLaunchKernelGGL((k_lone_gcm<SUITE, false>), lgrid, lblock, 0, s, kt->d_slots, \
-                                   kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res);        \
+                                   kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, lst);   \
         } else if (bpl_gcm == 1) {                                                             \
             QPP_LAUNCH_GCM_B(SUITE, 1);                                                         \
         } else {                                                                               \
@@ -2508,10 +2567,10 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     if ((mask & (1u << QPP_CHACHA20_POLY1305)) && lone && n <= lone_max(QPP_CHACHA20_POLY1305)) {
         if (enc)
             hipLaunchKernelGGL((k_lone_chacha<true>), lgrid, lblock, 0, s, kt->d_slots, kt->cap, d_desc, n, d_in,
-                               d_out, d_res);
+                               d_out, d_res, lst);
         else
             hipLaunchKernelGGL((k_lone_chacha<false>), lgrid, lblock, 0, s, kt->d_slots, kt->cap, d_desc, n, d_in,
-                               d_out, d_res);
+                               d_out, d_res, lst);
         HIPCHK(hipGetLastError());
     } else if (mask & (1u << QPP_CHACHA20_POLY1305)) {
         const dim3 grid((waves + kChachaWG / 64 - 1) / (kChachaWG / 64)), block(kChachaWG);
@@ -2893,14 +2952,20 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
         memset(h + sd + si, 0, out_len);  // bytes the kernel does not write come back as zeros
         if (n <= std::min(lone_max(QPP_AES_128_GCM), lone_max(QPP_CHACHA20_POLY1305)) && lone_choice() &&
             zero_copy_choice()) {
-            // one wave per packet: descriptors and input by one copy, the
-            // output and results written by the kernel straight into the
-            // pinned staging (PCIe writes post; reads there would put a bus
-            // round trip on each of the kernel's dependent loads)
-            HIPCHK(hipMemcpyAsync(d, h, sd + si, hipMemcpyHostToDevice, s->stream));
+            // one wave per packet; the output and results are written by
+            // the kernel straight into the pinned staging (PCIe writes post;
+            // reads there would put a bus round trip on each of the kernel's
+            // dependent loads).  Descriptors and input: copied by the kernel
+            // itself in one round trip when the call fits one workgroup,
+            // else by one copy
             uint8_t *dh = s->hd_in;
+            LoneStage st{dh, d, 0u};
+            if (n <= (uint32_t)(kLoneWG / 64) && sd + si <= kLoneStageMax && lone_stage_choice())
+                st.bytes = (uint32_t)(sd + si);  // 256-byte multiples
+            else
+                HIPCHK(hipMemcpyAsync(d, h, sd + si, hipMemcpyHostToDevice, s->stream));
             rc = launch_packets(enc, kt, (const qpp_desc *)d, n, d + sd, dh + sd + si,
-                                (qpp_result *)(dh + sd + si + so), s->stream);
+                                (qpp_result *)(dh + sd + si + so), s->stream, nullptr, &st);
             if (rc != QPP_OK) return rc;
             HIPCHK(hipStreamSynchronize(s->stream));
             if (out_len) memcpy(out, h + sd + si, out_len);

@@ -232,17 +232,19 @@ def test_lone_in_place(oracle, L):
         assert back[o : o + len(headers[i]) + len(payloads[i])].tobytes() == headers[i] + payloads[i], i
 
 
-def test_lone_through_staging_copies():
-    """The same small host calls with QPP_ZERO_COPY=0 (the session's staged
-    copies instead of the kernel reading and writing pinned memory), in a
-    child process, against the oracle."""
+@pytest.mark.parametrize("switch", ["QPP_ZERO_COPY", "QPP_LONE_STAGE"])
+def test_lone_through_staging_copies(switch):
+    """The same small host calls with QPP_ZERO_COPY=0 (both copies of the
+    session's staging, no writes into pinned memory from the kernel) or
+    QPP_LONE_STAGE=0 (the input by a copy instead of the kernel's own staging
+    read), in a child process, against the oracle."""
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = ("import sys; sys.path.insert(0, %r); from tests.test_gpu_lone import _child_check; _child_check()" % root)
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, QPP_ZERO_COPY="0"),
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **{switch: "0"}),
                        capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "lone child ok" in r.stdout
