@@ -277,6 +277,9 @@ struct LdsTe {
     __device__ __forceinline__ uint32_t addr(uint32_t s) const
     {
         // bytes {S0=s, S1=lo}: result byte0 = lo.byte0, byte1 = s.byte R, bytes 2,3 = 0
+        // (round 4: byte 1 as (s & 0xff00) | lo, one v_and_or_b32 instead of
+        // the v_perm, measured -0.3 % at the north star, -1.2 % config 2,
+        // +0.6 % config 4 on one box, profiles/r4s_ab_addr_andor.txt: kept)
         return __builtin_amdgcn_perm(s, lo, 0x0c0c0000u | ((4u + R) << 8));
     }
     __device__ __forceinline__ uint32_t t0(uint32_t s) const
