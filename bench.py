@@ -423,10 +423,11 @@ def main():
     if args.layout != "arrival":
         cfg["name"] += f" [{args.layout} layout]"
     bucketed = cfg.get("order", "grouped") != "grouped"
-    # the CPU baselines run before anything touches the GPU (they fork); at
-    # N > 1 rank 0 times them while the other ranks wait at the first barrier
+    # the CPU baselines run before anything touches the GPU (they fork), on
+    # rank 0 of an N = 1 run only (the same host and sample at every N; a
+    # scaling run's line carries null)
     cpu = cpu_all = None
-    if rank == 0 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(w, args.cpu_seconds, cfg, 1)
         if args.cpu_all_cores:
             cpu_all = cpu_baseline(w, max(2.0, args.cpu_seconds / 2), cfg, cpu_share())
