@@ -298,3 +298,46 @@ def _quad_child():
     headers, payloads, pns, slots = _random_batch(rng, 120, 6, recs)
     _check_round_trip(orc, L, eng, recs, headers, payloads, pns, slots, rng)
     print("quad child ok")
+
+
+@pytest.mark.parametrize("suite,n", [(0, 8192), (0, 8193), (1, 4096), (2, 64), (2, 65)],
+                         ids=["aes128-8192-lone", "aes128-8193-quad", "aes256-4096-lone", "chacha-64-lone",
+                              "chacha-65-quad"])
+def test_lone_threshold_sizes_whole_batch(L, suite, n):
+    """Device launches on either side of the lone / quad thresholds
+    (launch_packets: 8192 AES-GCM, 64 ChaCha20-Poly1305 packets), every
+    packet in both directions against the reference's own _crypto
+    (tests/ref_crypto.py; the C oracle on a prefix without oracle/_ref)."""
+    import torch
+
+    from aioquic_amd import bench_data
+    from aioquic_amd.batch import PacketEngine
+    from tests import ref_crypto
+
+    w = bench_data.make_workload(n, suite=suite, n_keys=3, seed=0x7E + n, order="random")
+    eng = PacketEngine(w.n_keys)
+    eng.set_key_records(w.keys)
+    dev = torch.device("cuda")
+    d_in = torch.from_numpy(w.plain).to(dev)
+    d_wire = torch.zeros(w.wire_size, dtype=torch.uint8, device=dev)
+    d_back = torch.zeros(w.plain_size, dtype=torch.uint8, device=dev)
+    d_res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_res2 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    eng.protect(torch.from_numpy(w.desc.view(np.uint8)).to(dev), n, d_in, d_wire, d_res)
+    eng.unprotect(torch.from_numpy(w.udesc.view(np.uint8)).to(dev), n, d_wire, d_back, d_res2)
+    torch.cuda.synchronize()
+    wire, back = d_wire.cpu().numpy(), d_back.cpu().numpy()
+    r1, r2 = d_res.cpu().numpy().view(L.RESULT), d_res2.cpu().numpy().view(L.RESULT)
+    assert (r1["status"] == 0).all() and (r2["status"] == 0).all()
+    assert np.array_equal(back, w.plain)
+    ref = ref_crypto.load()
+    if ref is not None:
+        assert np.array_equal(ref_crypto.protect_all(ref, w), wire)
+        r_back, r_pn = ref_crypto.unprotect_all(ref, w, wire)
+        assert np.array_equal(r_back, back) and np.array_equal(r_pn, r2["pn"])
+    else:
+        from oracle import oracle as orc
+
+        m = min(n, 512)
+        o_wire, _ = orc.protect_batch(w.keys, w.desc[:m], w.plain, w.wire_size)
+        assert np.array_equal(o_wire[: m * 1200], wire[: m * 1200])
