@@ -19,7 +19,8 @@ def main():
     from aioquic_amd import bench_data
     from aioquic_amd.batch import PacketEngine
 
-    mode = "quad" if os.environ.get("QPP_LONE") == "0" else "lone(max %s)" % os.environ.get("QPP_LONE_MAX", "16")
+    mode = ("quad" if os.environ.get("QPP_LONE") == "0" else
+            "lone(max %s)" % os.environ["QPP_LONE_MAX"] if "QPP_LONE_MAX" in os.environ else "default thresholds")
     dev = torch.device("cuda")
     sizes = [int(x) for x in os.environ.get("LONE_SIZES", "1,4,16,64,256,1024,4096").split(",")]
     for suite in [int(x) for x in os.environ.get("LONE_SUITES", "0,2").split(",")]:
