@@ -71,14 +71,26 @@ struct __attribute__((aligned(16))) ChachaSmem {
 };
 
 // Fill the LDS AES image: row x = [Te0[x] x 32 | Te1[x] x 32], 16-byte stores.
+// Every thread's table reads are issued before the first LDS store, so the
+// fill costs one memory round trip, not one per 16-byte store per thread.
 template <int NT>
 __device__ __forceinline__ void load_te(uint8_t *te)
 {
-    for (int i = threadIdx.x; i < 256 * 16; i += NT) {
-        const int x = i >> 4, part = i & 15;
-        const uint32_t v0 = c_aes.te0[x];
-        const uint32_t v = part < 8 ? v0 : rotl(v0, 8);
-        *(u32x4 *)(te + x * 256 + part * 16) = u32x4{v, v, v, v};
+    constexpr int kIters = (256 * 16 + NT - 1) / NT;
+    uint32_t v0[kIters];
+#pragma unroll
+    for (int k = 0; k < kIters; ++k) {
+        const int i = (int)threadIdx.x + k * NT;
+        v0[k] = i < 256 * 16 ? c_aes.te0[i >> 4] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kIters; ++k) {
+        const int i = (int)threadIdx.x + k * NT;
+        if (i < 256 * 16) {
+            const int x = i >> 4, part = i & 15;
+            const uint32_t v = part < 8 ? v0[k] : rotl(v0[k], 8);
+            *(u32x4 *)(te + x * 256 + part * 16) = u32x4{v, v, v, v};
+        }
     }
 }
 
@@ -1742,12 +1754,14 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
     const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
     const bool live = p < n;
     qpp_desc d = {0, 0, 0, 0, 0, 0, kNoSlot, 0};
+    QPP_PROBE_AT(kProbeStart);
     if (st.bytes) {
         // the call's bytes in flight beside the AES image build
         u32x4 a, b;
         lone_stage_load(st, a, b);
         load_te<kLoneWG>(te);
         lone_stage_store(st, a, b);
+        QPP_PROBE_AT(0);  // staging read, AES image
         __syncthreads();
         if (live) d = desc[p];
     } else {
@@ -1756,12 +1770,15 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         load_te<kLoneWG>(te);
         __syncthreads();
     }
+    QPP_PROBE_AT(1);  // barrier, descriptor
     if (!live || !lone_slot<SUITE>(d, slots, cap, res, p)) return;
+    QPP_PROBE_AT(2);  // the slot's suite
     const KeySlot *ks = slots + d.slot;
     const uint32_t lane = lane_fresh();
     const LdsTe T{te, (lane & 31) * 4};
     const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
     Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
+    QPP_PROBE_AT(3);  // header, pkt_begin (unprotect: header protection)
     if (P.status == QPP_S_OK) {
         const int hlen = P.hlen, clen = P.clen;
         const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, m = n_a + n_c + 1;
@@ -1785,6 +1802,7 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         for (int i = 0; i < 4 * (kNR + 1); ++i)
             rk[i] = __builtin_amdgcn_readfirstlane((i >= 12 && i < 4 * kNR) ? ks->rkr[i] : ks->rk[i]);
         const CtrCache cc = ctr_cache(P.nonce, rk, T);
+        QPP_PROBE_AT(4);  // inputs and powers requested, round keys, counter cache
         // CT block i: counter i + 2; the lengths position: J0 (counter 1)
         auto ctr = [&](int pos) -> uint32_t {
             return (pos >= n_a && pos < n_a + n_c) ? (uint32_t)(pos - n_a + 2) : 1u;
@@ -1811,12 +1829,15 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         };
         u32x4 ks0, ks1;
         aes_ctr2<kNR>(cc, ctr(pos0), ctr(pos1), rk, T, ks0, ks1);
+        QPP_PROBE_AT(5);  // AES-CTR
         const u32x4 x0 = out(pos0, in0, ks0), x1 = out(pos1, in1, ks1);
+        QPP_PROBE_AT(6);  // output stores, the inputs' wait
         u32x4 y = gf_mul(x0, h0) ^ gf_mul(x1, h1);
         for (int pos = (int)lane + 128; pos < m; pos += 64)  // > 128 blocks
             y ^= gf_mul(out(pos, input(pos), aes_ctr<kNR>(cc, ctr(pos), rk, T)), power(pos));
         const u32x4 tag = u32x4{wave_xor_u32(y.x), wave_xor_u32(y.y), wave_xor_u32(y.z), wave_xor_u32(y.w)} ^
                           readlane4(ej0, (m - 1) & 63);
+        QPP_PROBE_AT(7);  // GHASH (powers' wait, multiplies, wave xor)
         if (ENC) {
             if (lane == 0) st16(dst + hlen + clen, tag);
             if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[wv], tag, T);
@@ -1829,7 +1850,9 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
             }
         }
     }
+    QPP_PROBE_AT(8);  // header protection, tag, header
     write_result<ENC>(res, p, (int)lane_fresh(), P);
+    QPP_PROBE_AT(9);  // result
 }
 
 // One ChaCha20-Poly1305 packet per wave (RFC 8439 sec. 2.8).  Lane 0: the
