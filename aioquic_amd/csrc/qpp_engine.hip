@@ -1626,6 +1626,7 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
 // of 16 packets per CU), so unplanned launches up to lone_max take these
 // kernels; past that the quad kernels' ~7x fewer instructions per packet win.
 constexpr int kLoneWG = 1024;      // 16 packets per workgroup, one AES image
+constexpr int kLoneSpin = 1 << 18;  // pair launches: the first wave's bounded wait
 
 // A small host call handed to a lone kernel whole (qpp_session): the kernel
 // copies the call's descriptors and input from the pinned staging (src, its
@@ -1708,16 +1709,20 @@ __device__ __forceinline__ bool lone_slot(const qpp_desc &d, const KeySlot *slot
 // the mask by every quad, the header out by the lanes of its blocks.
 template <int SUITE, class TE>
 __device__ __forceinline__ void lone_protect_hp(Pkt &P, const KeySlot *ks, uint8_t *scr, u32x4 tag,
-                                                const TE &T)
+                                                const TE &T, bool have_mask = false, u32x4 mask = {0, 0, 0, 0})
 {
     const uint32_t lane = lane_fresh();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    if (P.clen < 32 && lane == 0)
-        for (int j = 0; j < 16 && P.clen + j < 32; ++j) scr[P.clen + j] = (uint8_t)byte_of(tag, j);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    P.mask = hp_mask_quad<SUITE>(ks, lds_sample(scr, 4 - P.pn_len), T, (int)(lane & 3));
+    if (have_mask) {
+        P.mask = mask;  // computed by the caller from the ciphertext
+    } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (P.clen < 32 && lane == 0)
+            for (int j = 0; j < 16 && P.clen + j < 32; ++j) scr[P.clen + j] = (uint8_t)byte_of(tag, j);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        P.mask = hp_mask_quad<SUITE>(ks, lds_sample(scr, 4 - P.pn_len), T, (int)(lane & 3));
+    }
     const int n_a = (P.hlen + 15) >> 4;
     for (int q = (int)lane; q < n_a; q += 64) {
         const int nb = min(16, P.hlen - 16 * q);
@@ -1738,6 +1743,11 @@ __device__ __forceinline__ u32x4 gf_mul(u32x4 x, u32x4 y)
 // blocks: long associated data): every load is issued before the first
 // use, both counter blocks run as one aes_ctr2 chain, and the two GHASH
 // terms are independent table-free multiplies (qpp_gf128.h).
+// A protect launch of at most 8 packets (the object API's calls) gives each
+// packet two waves instead ("pair"): wave 2k + h takes positions 64 h + l
+// (+ 128 j), so a lane multiplies once where one wave would multiply twice,
+// and wave 2k computes the header-protection mask while wave 2k + 1 finishes
+// its multiplies; wave 2k + 1 hands its share of the tag over through LDS.
 template <int SUITE, bool ENC>
 // (desc is not __restrict__: with a staged call it is the copy this kernel
 // writes, so its loads must not move above the staging)
@@ -1750,11 +1760,18 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
     constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
     __shared__ __attribute__((aligned(16))) uint8_t te[kTeBytes];
     __shared__ __attribute__((aligned(16))) uint8_t scr[kLoneWG / 64][48];
+    // pair launches: the second wave's share of a packet's tag, and its flag
+    __shared__ u32x4 xch[kLoneWG / 128];
+    __shared__ uint32_t xflag[kLoneWG / 128];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
+    const bool pair = ENC && n <= (uint32_t)(kLoneWG / 128);  // uniform over the launch
+    const int part = pair ? (int)(wv & 1u) : 0;
+    const uint32_t ps = pair ? wv >> 1 : wv;  // the packet's index in the workgroup
+    const uint32_t p = pair ? ps : blockIdx.x * (kLoneWG / 64) + wv;  // (pair: one workgroup)
     const bool live = p < n;
     qpp_desc d = {0, 0, 0, 0, 0, 0, kNoSlot, 0};
     QPP_PROBE_AT(kProbeStart);
+    if (threadIdx.x < kLoneWG / 128) xflag[threadIdx.x] = 0u;
     if (st.bytes) {
         // the call's bytes in flight beside the AES image build
         u32x4 a, b;
@@ -1795,7 +1812,8 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
             return zero4();
         };
         auto power = [&](int pos) -> u32x4 { return pos < m ? ld16(hpw + 16 * (m - 1 - pos)) : zero4(); };
-        const int pos0 = (int)lane, pos1 = (int)lane + 64;
+        const int stride = pair ? 128 : 64;
+        const int pos0 = (int)lane + 64 * part, pos1 = pos0 + stride;
         const u32x4 in0 = input(pos0), in1 = input(pos1), h0 = power(pos0), h1 = power(pos1);
         uint32_t rk[4 * (kNR + 1)];
 #pragma unroll
@@ -1820,7 +1838,7 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
                 const u32x4 o = in ^ ksb;
                 st_part(dst + hlen + 16 * i, o, nb);
                 x = keep_bytes(ENC ? o : in, nb);
-                if (ENC && P.hp && i < 2) *(u32x4 *)(scr[wv] + 16 * i) = x;
+                if (ENC && P.hp && i < 2) *(u32x4 *)(scr[ps] + 16 * i) = x;
             } else if (pos == m - 1) {
                 x = u32x4{0u, bswap((uint32_t)hlen * 8u), 0u, bswap((uint32_t)clen * 8u)};
                 ej0 = ksb;
@@ -1832,15 +1850,56 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         QPP_PROBE_AT(5);  // AES-CTR
         const u32x4 x0 = out(pos0, in0, ks0), x1 = out(pos1, in1, ks1);
         QPP_PROBE_AT(6);  // output stores, the inputs' wait
-        u32x4 y = gf_mul(x0, h0) ^ gf_mul(x1, h1);
-        for (int pos = (int)lane + 128; pos < m; pos += 64)  // > 128 blocks
+        // pair, first wave: the header-protection mask from CT blocks 0-1
+        // (its lanes n_a, n_a + 1) before the multiplies, beside the second
+        // wave's; otherwise after the tag (lone_protect_hp)
+        const bool hp_early = pair && part == 0 && P.hp && clen >= 20 && n_a + 1 < 64;
+        u32x4 hp_mask = zero4();
+        if (hp_early) {
+            const int na = __builtin_amdgcn_readfirstlane(n_a), sh = 4 - P.pn_len;
+            const u32x4 c0 = readlane4(x0, na), c1 = readlane4(x0, na + 1);
+            const u32x4 smp = {__builtin_amdgcn_alignbyte(c0.y, c0.x, sh), __builtin_amdgcn_alignbyte(c0.z, c0.y, sh),
+                               __builtin_amdgcn_alignbyte(c0.w, c0.z, sh), __builtin_amdgcn_alignbyte(c1.x, c0.w, sh)};
+            hp_mask = hp_mask_quad<SUITE>(ks, smp, T, (int)(lane & 3));
+        }
+        u32x4 y = gf_mul(x0, h0);
+        // the second term only where some lane holds a second position
+        if (__builtin_amdgcn_ballot_w64(pos1 < m) != 0) y ^= gf_mul(x1, h1);
+        for (int pos = pos1 + stride; pos < m; pos += stride)  // long associated data
             y ^= gf_mul(out(pos, input(pos), aes_ctr<kNR>(cc, ctr(pos), rk, T)), power(pos));
-        const u32x4 tag = u32x4{wave_xor_u32(y.x), wave_xor_u32(y.y), wave_xor_u32(y.z), wave_xor_u32(y.w)} ^
-                          readlane4(ej0, (m - 1) & 63);
+        // (the lane of position m - 1 holds E_K(J0) in its wave; zero elsewhere)
+        u32x4 tag = u32x4{wave_xor_u32(y.x), wave_xor_u32(y.y), wave_xor_u32(y.z), wave_xor_u32(y.w)} ^
+                    readlane4(ej0, (m - 1) & 63);
+        if (pair) {
+            if (part == 1) {
+                // hand the share over (and CT blocks 0-1 in scr, if this wave
+                // wrote them), then leave the packet to the first wave
+                if (lane == 0) xch[ps] = tag;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(&xflag[ps], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return;
+            }
+            // bounded wait (the second wave runs the same packet to here;
+            // kLoneSpin sleeps are milliseconds, a watchdog, never reached)
+            bool got = false;
+            for (int it = 0; it < kLoneSpin && !got; ++it) {
+                got = __hip_atomic_load(&xflag[ps], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
+                if (!got) __builtin_amdgcn_s_sleep(2);
+            }
+            asm volatile("" ::: "memory");
+            if (got) {
+                tag ^= xch[ps];
+            } else {
+                P.status = QPP_S_LENGTH;
+                if (lane == 0) atomicAdd(&g_qpp_watchdog, 1u);
+            }
+        }
         QPP_PROBE_AT(7);  // GHASH (powers' wait, multiplies, wave xor)
         if (ENC) {
-            if (lane == 0) st16(dst + hlen + clen, tag);
-            if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[wv], tag, T);
+            if (P.status == QPP_S_OK) {
+                if (lane == 0) st16(dst + hlen + clen, tag);
+                if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[ps], tag, T, hp_early, hp_mask);
+            }
         } else {
             const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
             if ((diff.x | diff.y | diff.z | diff.w) != 0) {
