@@ -1743,11 +1743,14 @@ __device__ __forceinline__ u32x4 gf_mul(u32x4 x, u32x4 y)
 // blocks: long associated data): every load is issued before the first
 // use, both counter blocks run as one aes_ctr2 chain, and the two GHASH
 // terms are independent table-free multiplies (qpp_gf128.h).
-// A protect launch of at most 8 packets (the object API's calls) gives each
-// packet two waves instead ("pair"): wave 2k + h takes positions 64 h + l
-// (+ 128 j), so a lane multiplies once where one wave would multiply twice,
-// and wave 2k computes the header-protection mask while wave 2k + 1 finishes
-// its multiplies; wave 2k + 1 hands its share of the tag over through LDS.
+// A launch of at most 8 packets (the object API's calls) gives each packet
+// two waves instead ("pair"): wave 2k + h takes positions 64 h + l
+// (+ 128 j), so a lane multiplies once where one wave would multiply twice;
+// wave 2k + 1 hands its share of the tag over through LDS.  Protect: wave 2k
+// computes the header-protection mask while wave 2k + 1 finishes its
+// multiplies.  Unprotect: wave 2k hands the verdict back, and on a failed tag
+// each wave zeroes the plaintext blocks it wrote (stores of one wave to one
+// address stay in order; another wave's could overtake them).
 template <int SUITE, bool ENC>
 // (desc is not __restrict__: with a staged call it is the copy this kernel
 // writes, so its loads must not move above the staging)
@@ -1764,7 +1767,7 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
     __shared__ u32x4 xch[kLoneWG / 128];
     __shared__ uint32_t xflag[kLoneWG / 128];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool pair = ENC && n <= (uint32_t)(kLoneWG / 128);  // uniform over the launch
+    const bool pair = n <= (uint32_t)(kLoneWG / 128);  // uniform over the launch
     const int part = pair ? (int)(wv & 1u) : 0;
     const uint32_t ps = pair ? wv >> 1 : wv;  // the packet's index in the workgroup
     const uint32_t p = pair ? ps : blockIdx.x * (kLoneWG / 64) + wv;  // (pair: one workgroup)
@@ -1870,24 +1873,36 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         // (the lane of position m - 1 holds E_K(J0) in its wave; zero elsewhere)
         u32x4 tag = u32x4{wave_xor_u32(y.x), wave_xor_u32(y.y), wave_xor_u32(y.z), wave_xor_u32(y.w)} ^
                     readlane4(ej0, (m - 1) & 63);
+        // a wave's plaintext blocks, zeroed after a failed tag (unprotect)
+        auto wipe_own = [&]() {
+            for (int pos = pos0; pos < m; pos += stride) {
+                const int i = pos - n_a;
+                if (i >= 0 && i < n_c) st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
+            }
+        };
+        // bounded waits on xflag (the other wave runs the same packet to its
+        // hand-over; kLoneSpin sleeps are milliseconds, a watchdog, never reached)
+        auto wait_flag = [&](uint32_t below) -> uint32_t {
+            uint32_t f = 0u;
+            for (int it = 0; it < kLoneSpin; ++it) {
+                f = __hip_atomic_load(&xflag[ps], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (f >= below) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            asm volatile("" ::: "memory");
+            return f;
+        };
         if (pair) {
             if (part == 1) {
                 // hand the share over (and CT blocks 0-1 in scr, if this wave
-                // wrote them), then leave the packet to the first wave
+                // wrote them); unprotect: wait for the verdict (2 ok, 3 failed)
                 if (lane == 0) xch[ps] = tag;
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store(&xflag[ps], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return;
+                if (!ENC && wait_flag(2u) == 3u) wipe_own();
+                return;  // the first wave writes the result
             }
-            // bounded wait (the second wave runs the same packet to here;
-            // kLoneSpin sleeps are milliseconds, a watchdog, never reached)
-            bool got = false;
-            for (int it = 0; it < kLoneSpin && !got; ++it) {
-                got = __hip_atomic_load(&xflag[ps], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
-                if (!got) __builtin_amdgcn_s_sleep(2);
-            }
-            asm volatile("" ::: "memory");
-            if (got) {
+            if (wait_flag(1u) >= 1u) {
                 tag ^= xch[ps];
             } else {
                 P.status = QPP_S_LENGTH;
@@ -1902,10 +1917,12 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
             }
         } else {
             const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
-            if ((diff.x | diff.y | diff.z | diff.w) != 0) {
-                P.status = QPP_S_DECRYPT;
-                for (int i = (int)lane - n_a; i < n_c; i += 64)
-                    if (i >= 0) st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
+            const bool bad = (diff.x | diff.y | diff.z | diff.w) != 0 || P.status != QPP_S_OK;
+            if (pair && lane == 0)
+                __hip_atomic_store(&xflag[ps], bad ? 3u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (bad) {
+                if (P.status == QPP_S_OK) P.status = QPP_S_DECRYPT;
+                wipe_own();
             }
         }
     }

@@ -64,6 +64,13 @@ def _check_round_trip(oracle, L, eng, recs, headers, payloads, pns, slots, rng, 
                 o, ln = int(ud[j]["out_off"]), int(r_g[j]["out_len"])
                 assert np.array_equal(u_g[o : o + ln], u_o[o : o + ln]), (sl, j)
                 n_ok += 1
+            elif r_g[j]["status"] == L.S_DECRYPT:
+                # no plaintext after a failed tag (launches of <= 8 packets
+                # split a packet over two waves, each zeroing its own blocks):
+                # past the longest header (pn offset + 4) up to the tag, zeros
+                o = int(ud[j]["out_off"])
+                lo, hi = o + int(ud[j]["hdr_len"]) + 4, o + int(ud[j]["len"]) - 16
+                assert not u_g[lo:hi].any(), (sl, j)
     return n_ok
 
 
