@@ -1948,20 +1948,25 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
     __shared__ __attribute__((aligned(16))) uint8_t scr[kLoneWG / 64][48];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * (kLoneWG / 64) + wv;
+    QPP_PROBE_AT(kProbeStart);
     if (st.bytes) {
         u32x4 a, b;
         lone_stage_load(st, a, b);
         lone_stage_store(st, a, b);
+        QPP_PROBE_AT(0);  // staging read
         __syncthreads();
     }
     if (p >= n) return;
     const qpp_desc d = desc[p];
+    QPP_PROBE_AT(1);  // barrier, descriptor
     if (!lone_slot<SUITE>(d, slots, cap, res, p)) return;
+    QPP_PROBE_AT(2);  // the slot's suite
     const KeySlot *ks = slots + d.slot;
     const uint32_t lane = lane_fresh();
     const ConstTe T;
     const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
     Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
+    QPP_PROBE_AT(3);  // header, pkt_begin (unprotect: header protection)
     if (P.status == QPP_S_OK) {
         const int hlen = P.hlen, clen = P.clen;
         const int n_a = (hlen + 15) >> 4, n_c = (clen + 15) >> 4, m = n_a + n_c + 1;
@@ -1998,15 +2003,37 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
 #pragma unroll
         for (int w = 0; w < 8; ++w) key[w] = __builtin_amdgcn_readfirstlane(ks->rk[w]);
         uint32_t blk[16];
+        QPP_PROBE_AT(4);  // inputs requested, key
         chacha_block(key, lane, P.nonce.x, P.nonce.y, P.nonce.z, blk);
+        QPP_PROBE_AT(5);  // the ChaCha20 block
         uint32_t kw[8];
 #pragma unroll
         for (int w = 0; w < 8; ++w) kw[w] = (uint32_t)__builtin_amdgcn_readlane((int)blk[w], 0);
         const P130 r = p130_r(kw[0], kw[1], kw[2], kw[3]);
-        // r^e, e = m - (q + cnt - 1), beside the Horner chain
-        const int e = cnt > 0 ? m - (q + cnt - 1) : 0;
-        P130 rp = r, re = p130_zero();
-        re.v[0] = 1u;
+        // r^e, e = m - (q + cnt - 1): lane j holds r^(j + 1) after an
+        // inclusive prefix product over the wave (6 multiplies per lane), a
+        // lane reads r^(1 + (e - 1) mod 64) from its lane by ds_bpermute and
+        // multiplies by r^64 (lane 63's) once per 64 -- 7-8 multiplies where
+        // square-and-multiply over 8 bits of e took 15
+        const P130 one = {{1u, 0u, 0u, 0u, 0u}};
+        P130 tp = r;
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            P130 u;
+#pragma unroll
+            for (int l = 0; l < 5; ++l) u.v[l] = (uint32_t)__shfl_up((int)tp.v[l], (unsigned)k);
+            tp = p130_mul(tp, (int)lane >= k ? u : one);
+        }
+        const int e = cnt > 0 ? m - (q + cnt - 1) : 1;
+        const int e1 = e - 1, hi = e1 >> 6;
+        P130 re, r64;
+#pragma unroll
+        for (int l = 0; l < 5; ++l) {
+            re.v[l] = (uint32_t)__shfl((int)tp.v[l], e1 & 63);
+            r64.v[l] = (uint32_t)__builtin_amdgcn_readlane((int)tp.v[l], 63);
+        }
+        for (int h = 1; h <= 3; ++h)  // e <= 1 + 3 * 64 + 63 (m <= 190)
+            if (__builtin_amdgcn_ballot_w64(hi >= h) != 0) re = p130_mul(re, hi >= h ? r64 : one);
         const bool masked = !ENC && P.hp;
         P130 w = p130_zero();
 #pragma unroll
@@ -2032,17 +2059,14 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
             // than it has only multiplies zero)
             const P130 mb = p130_block(x);
             if (b < cnt) w = p130_add(b == 0 ? w : p130_mul(w, r), mb);
-            // two steps of the power chain per block step (8 bits of e)
-            re = p130_mul(re, ((e >> (2 * b)) & 1) ? rp : P130{{1u, 0u, 0u, 0u, 0u}});
-            rp = p130_mul(rp, rp);
-            re = p130_mul(re, ((e >> (2 * b + 1)) & 1) ? rp : P130{{1u, 0u, 0u, 0u, 0u}});
-            if (b < 3) rp = p130_mul(rp, rp);
         }
+        QPP_PROBE_AT(6);  // Horner and r^e, outputs
         w = p130_mul(w, re);
         P130 sum;
 #pragma unroll
         for (int l = 0; l < 5; ++l) sum.v[l] = wave_sum_u32(w.v[l]);
         const u32x4 tag = p130_finish(sum, kw[4], kw[5], kw[6], kw[7]);
+        QPP_PROBE_AT(7);  // scaling multiply, wave sum, tag
         if (ENC) {
             if (lane == 0) st16(dst + hlen + clen, tag);
             if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[wv], tag, T);
@@ -2058,7 +2082,9 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
             }
         }
     }
+    QPP_PROBE_AT(8);  // header protection, tag, header
     write_result<ENC>(res, p, (int)lane_fresh(), P);
+    QPP_PROBE_AT(9);  // result
 }
 
 // Header-protection masks only (HeaderProtection_mask, _crypto.c:278-287).

@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/$TAG; mkdir -p $O
 [ -n "${NOTEST:-}" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -60 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
-timeout -k 10 120 tools/lone_probe 400 > $O/lone_probe.txt 2>&1 || { echo "lone_probe failed"; cat $O/lone_probe.txt; exit 1; }
+timeout -k 10 120 tools/lone_probe 400 ${PROBE_SUITE:-0} > $O/lone_probe.txt 2>&1 || { echo "lone_probe failed"; cat $O/lone_probe.txt; exit 1; }
 cat $O/lone_probe.txt
 lp_of() { [[ $1 == new ]] && echo "" || echo "$PWD/variants/$1"; }
 for rep in 1 2 3; do

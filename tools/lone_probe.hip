@@ -1,10 +1,10 @@
-// Phase times of the one-packet kernel (k_lone_gcm) on the object API's path:
-// the engine built with -DQPP_PROBE, qpp_session_protect / _unprotect of one
-// 1200-byte AES-128-GCM packet per call (the call staged by the kernel), wave
-// 0's marks averaged over the calls.
+// Phase times of the one-packet kernels (k_lone_gcm, k_lone_chacha) on the
+// object API's path: the engine built with -DQPP_PROBE, qpp_session_protect /
+// _unprotect of one 1200-byte packet per call (the call staged by the
+// kernel), wave 0's marks averaged over the calls.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -DQPP_PROBE -c -o /tmp/lone_probe.o tools/lone_probe.hip && \
 //        hipcc --offload-arch=gfx950 -o tools/lone_probe /tmp/lone_probe.o build/obj/qpp_plan.o
-// Run:   tools/lone_probe [calls]
+// Run:   tools/lone_probe [calls] [suite: 0 AES-128-GCM, 2 ChaCha20-Poly1305]
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -16,6 +16,12 @@
 constexpr int kProbeSlots = 16, kProbeStart = 13, kProbeEnd = 14;
 #endif
 
+static const char *kNamesChacha[] = {"staging read", "barrier, descriptor", "the slot's suite",
+                                     "header, pkt_begin (unprotect: HP removal)", "inputs requested, key",
+                                     "the ChaCha20 block", "Horner and r^e (prefix product), outputs",
+                                     "scaling multiply, wave sum, tag",
+                                     "protect: HP, tag, header / unprotect: tag check", "result"};
+static const char *const *g_names;
 static const char *kNames[] = {"staging read, AES image", "barrier, descriptor", "the slot's suite",
                                "header, pkt_begin (unprotect: HP removal)",
                                "inputs/powers requested, round keys, counter cache", "AES-CTR",
@@ -60,21 +66,23 @@ static int run(qpp_session *s, qpp_keytab *kt, bool enc, int calls, std::vector<
     }
     printf("%s, wave 0, mean of %d calls: start to last mark %.2f us\n", enc ? "protect" : "unprotect", n_ok,
            span / n_ok);
-    for (int ph = 0; ph < 10; ++ph) printf("  %-52s %6.2f us\n", kNames[ph], sum[ph] / n_ok);
+    for (int ph = 0; ph < 10; ++ph) printf("  %-52s %6.2f us\n", g_names[ph], sum[ph] / n_ok);
     return 0;
 }
 
 int main(int argc, char **argv)
 {
     const int calls = argc > 1 ? atoi(argv[1]) : 300;
+    const int suite = argc > 2 ? atoi(argv[2]) : QPP_AES_128_GCM;
+    g_names = suite == QPP_CHACHA20_POLY1305 ? kNamesChacha : kNames;
     qpp_keytab *kt = nullptr;
     qpp_session *s = nullptr;
     if (qpp_keytab_create(4, &kt) != QPP_OK || qpp_session_create(1 << 16, 64, &s) != QPP_OK) return 1;
     qpp_key_material km = {};
     km.slot = 0;
-    km.suite = QPP_AES_128_GCM;
+    km.suite = (uint8_t)suite;
     for (int i = 0; i < 12; ++i) km.iv[i] = (uint8_t)(i + 1);
-    for (int i = 0; i < 16; ++i) km.key[i] = (uint8_t)(3 * i), km.hp[i] = (uint8_t)(5 * i + 1);
+    for (int i = 0; i < 32; ++i) km.key[i] = (uint8_t)(3 * i), km.hp[i] = (uint8_t)(5 * i + 1);
     if (qpp_session_set_keys(s, kt, &km, 1) != QPP_OK) return 1;
     std::vector<uint8_t> pkt;
     if (run(s, kt, true, calls, pkt) || run(s, kt, false, calls, pkt)) return 1;
