@@ -1708,8 +1708,11 @@ __device__ __forceinline__ bool lone_slot(const qpp_desc &d, const KeySlot *slot
 // lanes of CT blocks 0 and 1 (and the tag, for ciphertexts under 32 bytes),
 // the mask by every quad, the header out by the lanes of its blocks.
 template <int SUITE, class TE>
+// own / own_ok: header block `lane` as the lane loaded it already (no reload
+// on the call's path); have_mask / mask: the mask computed by the caller.
 __device__ __forceinline__ void lone_protect_hp(Pkt &P, const KeySlot *ks, uint8_t *scr, u32x4 tag,
-                                                const TE &T, bool have_mask = false, u32x4 mask = {0, 0, 0, 0})
+                                                const TE &T, u32x4 own, bool own_ok, bool have_mask = false,
+                                                u32x4 mask = {0, 0, 0, 0})
 {
     const uint32_t lane = lane_fresh();
     if (have_mask) {
@@ -1726,7 +1729,8 @@ __device__ __forceinline__ void lone_protect_hp(Pkt &P, const KeySlot *ks, uint8
     const int n_a = (P.hlen + 15) >> 4;
     for (int q = (int)lane; q < n_a; q += 64) {
         const int nb = min(16, P.hlen - 16 * q);
-        u32x4 h = ld_win(P.src + 16 * q, nb, P.src, P.src + P.hlen + P.clen);
+        u32x4 h = (own_ok && q == (int)lane) ? keep_bytes(own, nb)
+                                              : ld_win(P.src + 16 * q, nb, P.src, P.src + P.hlen + P.clen);
         h ^= hp_pattern(16 * q, P.mask, P.fbm, P.pn_off, P.pn_len);
         st_part(P.dst + 16 * q, h, nb);
     }
@@ -1913,7 +1917,10 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         if (ENC) {
             if (P.status == QPP_S_OK) {
                 if (lane == 0) st16(dst + hlen + clen, tag);
-                if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[ps], tag, T, hp_early, hp_mask);
+                // (lane q of the first wave loaded header block q as its position q)
+                if (P.hp)
+                    lone_protect_hp<SUITE>(P, ks, scr[ps], tag, T, x0, part == 0 && (int)lane < n_a, hp_early,
+                                           hp_mask);
             }
         } else {
             const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
@@ -2069,7 +2076,8 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_chacha(const KeySlot *__restri
         QPP_PROBE_AT(7);  // scaling multiply, wave sum, tag
         if (ENC) {
             if (lane == 0) st16(dst + hlen + clen, tag);
-            if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[wv], tag, T);
+            // (header block 0: requested with the descriptor, pre.h0)
+            if (P.hp) lone_protect_hp<SUITE>(P, ks, scr[wv], tag, T, pre.h0, lane == 0 && hlen + clen >= 16);
         } else {
             const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
             if ((diff.x | diff.y | diff.z | diff.w) != 0) {
