@@ -82,8 +82,10 @@ class KeySlots:
     Like the reference's AEAD objects, a KeySlots is not meant to be shared
     by threads; the batched callers' default table is one per thread.  A
     release that another thread triggers (a context torn down there) is
-    queued and applied by the table's own thread at its next assign(), so
-    no thread changes another's table."""
+    queued and applied by the table's own thread at its next assign(),
+    commit(), release() or close(), so no thread changes another's table
+    (close() lets an owner that stops assigning apply the queue and free every
+    slot at once)."""
 
     def __init__(self, capacity: int = 1024) -> None:
         self.capacity = int(capacity)
@@ -128,6 +130,8 @@ class KeySlots:
 
     def commit(self) -> None:
         """Install the slots added since the last commit (one launch)."""
+        if self._inbox:
+            self._drain()
         if self._pending:
             self.table.set(np.concatenate(self._pending).tobytes())
             self._pending.clear()
@@ -150,6 +154,8 @@ class KeySlots:
     def release(self, objs) -> None:
         """Forget every slot built from one of `objs` (AEAD or HP objects)
         and clear those device entries."""
+        if self._inbox:
+            self._drain()
         dropped = set()
         for o in objs:
             for k in self._by_obj.pop(id(o), ()) if o is not None else ():
@@ -183,6 +189,15 @@ class KeySlots:
             todo, self._inbox = self._inbox, []
         for objs in todo:
             self.release(objs)
+
+    def close(self) -> None:
+        """The owner is done with the table: apply queued releases, then
+        clear every device entry still held and drop the held objects."""
+        self._drain()
+        held = sorted(self._keep)
+        if held:
+            self.table.clear(np.asarray(held, np.uint32).tobytes())
+        self.reset()
 
 
 # every live KeySlots, so that a context's teardown can release its keys;
@@ -228,6 +243,8 @@ def _raise_status(status: int) -> Exception:
         return CryptoError("Payload decryption failed")
     if status == L.S_NO_KEY:
         return KeyUnavailableError("Decryption key is not available")
+    if status == L.S_INTERNAL:
+        return CryptoError(L.INTERNAL_ERROR)
     return CryptoError("Invalid payload length")
 
 

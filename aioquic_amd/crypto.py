@@ -91,6 +91,8 @@ def _status_error(status: int) -> Exception:
         return KeyUnavailableError("Decryption key is not available")
     if status == L.S_DECRYPT:
         return CryptoError("Payload decryption failed")
+    if status == L.S_INTERNAL:
+        return CryptoError(L.INTERNAL_ERROR)
     return CryptoError("Invalid payload length")
 
 

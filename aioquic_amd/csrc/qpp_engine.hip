@@ -1188,9 +1188,17 @@ template <int WG>
 constexpr int gcm_tab_entries() { return WG == 512 ? 1 : kTabEntries; }
 static_assert(kGhLdsEntry % 1024 == 0, "LDS-DMA pieces of 1 KiB");
 
-// GCM table-entry watchdog events since the library loaded (tab_acquire gave
-// up: that slot's packets were skipped without results); never expected.
+// Watchdog events since the library loaded (tab_acquire gave up on a GHASH
+// table entry, or a pair launch's hand-over timed out: the packets concerned
+// report QPP_S_INTERNAL); never expected.
 __device__ uint32_t g_qpp_watchdog;
+
+// The bounded waits' limits, in sleep rounds: a GHASH table entry (tab_acquire;
+// ~1 s at 2^22) and a pair launch's hand-over (k_lone_gcm).  Read where they
+// are used, not kept in registers (an SGPR live across k_gcm's step loop
+// spills); the host lowers both only under QPP_SPIN_LIMIT, a test switch.
+__device__ uint32_t g_qpp_spin_tab = 1u << 22;
+__device__ uint32_t g_qpp_spin_lone = 1u << 18;
 
 template <int WG, int NE = gcm_tab_entries<WG>()>
 struct __attribute__((aligned(16))) GcmSmem {
@@ -1211,21 +1219,25 @@ struct __attribute__((aligned(16))) GcmSmem {
 
 // Entry of slot `cur` for the calling wave (wave-uniform control flow):
 // found, or loaded into a free entry.  Lane 0 does the bookkeeping under the
-// workgroup's LDS lock.  Returns once the entry's table is in LDS.  (Returning
+// workgroup's LDS lock.  Returns once the entry's table is in LDS, or kNoSlot
+// when `spin` rounds of waiting for a free entry, or for another wave's load
+// of the entry, ran out (a watchdog: the caller fails the slot's packets with
+// QPP_S_INTERNAL; QPP_SPIN_LIMIT=0 forces it in tests, g_qpp_spin_tab).  (Returning
 // before the table has landed, to overlap its LDS-DMA with the packets'
 // descriptors and headers, measured 2-4 % slower at 64 Ki: those loads queue
 // behind the DMA in the vector memory counter, profiles/r4d_ab_tab_defer.txt.)
 template <int WG>
 __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t cur)
 {
+    const uint32_t spin = __builtin_nontemporal_load(&g_qpp_spin_tab);
     typedef const __attribute__((address_space(1))) void *gptr_t;
     typedef __attribute__((address_space(3))) void *lptr_t;
     uint32_t e = kNoSlot, load = 0;
     // bounded: every entry in use means other waves are running their slots,
     // and each of them releases its entry when done (watchdog, not a limit
-    // that a correct run reaches: ~1 s of sleeps)
+    // that a correct run reaches: ~1 s of sleeps at the default 2^22)
 #pragma unroll 1
-    for (int spin = 0; spin < (1 << 22); ++spin) {
+    for (uint32_t it = 0; it < spin; ++it) {
         uint32_t got = kNoSlot, ld = 0;
         if (lane_fresh() == 0) {
             while (atomicCAS(&sm.lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
@@ -1266,7 +1278,7 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
         }
         __builtin_amdgcn_s_sleep(8);
     }
-    if (e == kNoSlot) return e;  // watchdog: no entry came free (the slot's packets are skipped)
+    if (e == kNoSlot) return e;  // watchdog: no entry came free
     if (load) {
         // H^4 of the slot in the step loop's layout: 14 pieces of 1 KiB
         const uint8_t *src = gtab + (size_t)cur * kGhashTabBytes + kGh5Off;
@@ -1278,10 +1290,20 @@ __device__ uint32_t tab_acquire(GcmSmem<WG> &sm, const uint8_t *gtab, uint32_t c
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane_fresh() == 0) lds_st(&sm.eready[e], 1u);
     } else {
+        bool ready = false;
 #pragma unroll 1
-        for (int spin = 0; spin < (1 << 22); ++spin) {
-            if (__builtin_amdgcn_readfirstlane(lds_ld(&sm.eready[e]))) break;
+        for (uint32_t it = 0; it < spin; ++it) {
+            if (__builtin_amdgcn_readfirstlane(lds_ld(&sm.eready[e]))) {
+                ready = true;
+                break;
+            }
             __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ready) {
+            // watchdog: the loading wave never published the table; drop the
+            // reference taken above rather than read a table not yet landed
+            if (lane_fresh() == 0) atomicSub(&sm.eref[e], 1u);
+            return kNoSlot;
         }
     }
     return e;
@@ -1459,17 +1481,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             const uint32_t held = __builtin_amdgcn_readfirstlane(lds_ld(&sm.wslot[wv]));
             const uint32_t suite =
                 cur == held ? (uint32_t)SUITE : __builtin_amdgcn_readfirstlane(slots[cur].suite);
+            // a status for every packet of the slot instead of running them
+            uint32_t fail = 0u;
             if (suite > QPP_CHACHA20_POLY1305) {
-                // an empty slot: KeyUnavailableError (every suite's launch writes the same)
-                if (s == cur && (t & 3) == 0) {
-                    const qpp_desc d = desc[p];
-                    res[planned ? d.rsv : p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
-                }
-                continue;
-            }
-            if (suite != SUITE) continue;  // another suite's launch
-            QPP_PROBE_AT(1);
-            if (cur != held) {
+                fail = QPP_S_NO_KEY;  // an empty slot: KeyUnavailableError (every suite's launch writes it)
+            } else if (suite != SUITE) {
+                continue;  // another suite's launch
+            } else if (cur != held) {
+                QPP_PROBE_AT(1);
                 // release before acquiring: a wave never waits holding an entry
                 if (held != kNoSlot) {
                     tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(lds_ld(&sm.went[wv])));
@@ -1478,17 +1497,22 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 const uint32_t e = tab_acquire<WG>(sm, gtab, cur);
                 if (e == kNoSlot) {
                     // the watchdog gave up: the slot's packets are not
-                    // processed.  Their results are not written (per-packet
-                    // reporting here costs the step loop registers), so the
-                    // launch counts the event for the host to read
-                    // (qpp_watchdog_count; the GPU test suite checks it).
+                    // processed and report QPP_S_INTERNAL (no stale result
+                    // from an earlier launch survives); the launch also
+                    // counts the event (qpp_watchdog_count)
                     if (lane_fresh() == 0) atomicAdd(&g_qpp_watchdog, 1u);
-                    continue;
-                }
-                if (lane_fresh() == 0) {
+                    fail = QPP_S_INTERNAL;
+                } else if (lane_fresh() == 0) {
                     lds_st(&sm.wslot[wv], cur);
                     lds_st(&sm.went[wv], e);
                 }
+            }
+            if (fail) {
+                if (s == cur && (t & 3) == 0) {
+                    const qpp_desc d = desc[p];
+                    res[planned ? d.rsv : p] = qpp_result{d.pn, (uint16_t)fail, 0, 0};
+                }
+                continue;
             }
             QPP_PROBE_AT(2);  // table entry
             run_slot(cur);
@@ -1626,7 +1650,6 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
 // of 16 packets per CU), so unplanned launches up to lone_max take these
 // kernels; past that the quad kernels' ~7x fewer instructions per packet win.
 constexpr int kLoneWG = 1024;      // 16 packets per workgroup, one AES image
-constexpr int kLoneSpin = 1 << 18;  // pair launches: the first wave's bounded wait
 
 // A small host call handed to a lone kernel whole (qpp_session): the kernel
 // copies the call's descriptors and input from the pinned staging (src, its
@@ -1884,32 +1907,63 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
                 if (i >= 0 && i < n_c) st_part(dst + hlen + 16 * i, zero4(), min(16, clen - 16 * i));
             }
         };
-        // bounded waits on xflag (the other wave runs the same packet to its
-        // hand-over; kLoneSpin sleeps are milliseconds, a watchdog, never reached)
+        // The hand-over's flag (pair launches), moved only by compare-and-swap
+        // so that a wave that gives up cannot be overwritten by the other:
+        // 0 start, 1 the second wave's share is in xch, 2 / 3 the first
+        // wave's verdict (unprotect: tag ok / failed), 4 the first wave gave
+        // up waiting for the share, 5 the second wave gave up waiting for the
+        // verdict.  Both waves are resident in one workgroup, so the bounded
+        // waits (g_qpp_spin_lone sleeps: milliseconds) are a watchdog that a
+        // correct run never reaches; when one fires, the packet reports
+        // QPP_S_INTERNAL and unprotect zeroes its plaintext on both sides.
+        auto flag_cas = [&](uint32_t from, uint32_t to) -> uint32_t {
+            uint32_t prev = from;
+            if (lane == 0)
+                __hip_atomic_compare_exchange_strong(&xflag[ps], &prev, to, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+            return __builtin_amdgcn_readfirstlane(prev);
+        };
         auto wait_flag = [&](uint32_t below) -> uint32_t {
             uint32_t f = 0u;
-            for (int it = 0; it < kLoneSpin; ++it) {
-                f = __hip_atomic_load(&xflag[ps], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t spin = __builtin_nontemporal_load(&g_qpp_spin_lone);
+            for (uint32_t it = 0; it < spin; ++it) {
+                f = __hip_atomic_load(&xflag[ps], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (f >= below) break;
                 __builtin_amdgcn_s_sleep(2);
             }
-            asm volatile("" ::: "memory");
-            return f;
+            return __builtin_amdgcn_readfirstlane(f);
         };
+        bool handed = false;  // first wave: the second wave's share arrived
         if (pair) {
             if (part == 1) {
                 // hand the share over (and CT blocks 0-1 in scr, if this wave
-                // wrote them); unprotect: wait for the verdict (2 ok, 3 failed)
+                // wrote them); the release orders those stores before the flag
                 if (lane == 0) xch[ps] = tag;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_store(&xflag[ps], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (!ENC && wait_flag(2u) == 3u) wipe_own();
+                const uint32_t prev = flag_cas(0u, 1u);
+                if (!ENC) {
+                    // unprotect: keep this wave's plaintext only on verdict 2
+                    uint32_t f = prev;
+                    if (prev == 0u) {
+                        f = wait_flag(2u);
+                        if (f < 2u) {
+                            const uint32_t q = flag_cas(1u, 5u);
+                            f = q == 1u ? 5u : q;
+                        }
+                    }
+                    if (f != 2u) wipe_own();
+                }
                 return;  // the first wave writes the result
             }
-            if (wait_flag(1u) >= 1u) {
+            uint32_t f = wait_flag(1u);
+            if (f < 1u) {
+                const uint32_t q = flag_cas(0u, 4u);
+                f = q == 0u ? 4u : q;
+            }
+            if (f == 1u) {
+                handed = true;
                 tag ^= xch[ps];
             } else {
-                P.status = QPP_S_LENGTH;
+                P.status = QPP_S_INTERNAL;
                 if (lane == 0) atomicAdd(&g_qpp_watchdog, 1u);
             }
         }
@@ -1924,9 +1978,14 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
             }
         } else {
             const u32x4 got = ld16(src + hlen + clen), diff = got ^ tag;
-            const bool bad = (diff.x | diff.y | diff.z | diff.w) != 0 || P.status != QPP_S_OK;
-            if (pair && lane == 0)
-                __hip_atomic_store(&xflag[ps], bad ? 3u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            bool bad = (diff.x | diff.y | diff.z | diff.w) != 0 || P.status != QPP_S_OK;
+            if (handed && flag_cas(1u, bad ? 3u : 2u) != 1u) {
+                // the second wave gave up waiting for the verdict (and wiped
+                // its blocks): the packet fails here too
+                P.status = QPP_S_INTERNAL;
+                bad = true;
+                if (lane == 0) atomicAdd(&g_qpp_watchdog, 1u);
+            }
             if (bad) {
                 if (P.status == QPP_S_OK) P.status = QPP_S_DECRYPT;
                 wipe_own();
@@ -2294,6 +2353,8 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -2601,6 +2662,30 @@ static bool lone_stage_choice()
     return b;
 }
 
+// QPP_SPIN_LIMIT (a test switch, read once per process) replaces the bounded
+// waits' limits (g_qpp_spin_tab, g_qpp_spin_lone) on each device before its
+// first launch: 0 makes every bounded wait give up at once, so the watchdog
+// paths' QPP_S_INTERNAL reporting can be checked.
+static int apply_spin_env(hipStream_t s)
+{
+    static const long env = [] {
+        const char *v = getenv("QPP_SPIN_LIMIT");
+        return v ? atol(v) : -1L;
+    }();
+    if (env < 0) return QPP_OK;
+    static std::atomic<uint64_t> done{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load() & bit) return QPP_OK;
+    const uint32_t v = (uint32_t)env;
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_qpp_spin_tab), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_qpp_spin_lone), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    done.fetch_or(bit);
+    return QPP_OK;
+}
+
 static uint32_t cu_count()
 {
     static int cus[64];
@@ -2648,6 +2733,7 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
     if (!kt || (n && (!d_desc || !d_in || !d_out || !d_res))) return QPP_E_ARG;
     if (n == 0) return QPP_OK;
     hipStream_t s = (hipStream_t)stream;
+    if (int rc = apply_spin_env(s)) return rc;
     // one launch per suite the table holds now; unplanned, an empty table
     // still gets one launch so every packet reports QPP_S_NO_KEY (planned,
     // the no-key bucket has its own kernel)
@@ -2959,6 +3045,142 @@ static int session_launch(bool enc, qpp_session *s, const qpp_keytab *kt, const 
     return rc;
 }
 
+// Registered host buffers (qpp_host_register): page-locked caller memory
+// that the pipelined session path moves by DMA directly.  Pinning works on
+// whole pages, and two small arrays may share a page, so a request is pinned
+// as up to three pieces -- its first page, its interior, its last page --
+// each a hipHostRegister of its own: only a boundary page can be shared with
+// another live array, and it is then one piece held by both (reference
+// count), while the interior belongs to the request alone and is unpinned
+// with it (so no pin outlives the memory it was taken on).  A transfer goes
+// direct when pieces cover it, cut at piece boundaries (one runtime
+// registration per copy).
+struct HostPiece {
+    uintptr_t lo, hi;
+    int refs;
+};
+struct HostReq {
+    uintptr_t key, lo, hi;
+};
+constexpr uintptr_t kPage = 4096;
+static std::mutex g_host_mu;
+static std::vector<HostPiece> g_pieces;  // disjoint, sorted by lo
+static std::vector<HostReq> g_reqs;
+
+// The pieces covering [a, b) in order, or empty when some byte is not pinned.
+static std::vector<std::pair<uintptr_t, uintptr_t>> host_cover(const void *p, size_t len)
+{
+    std::vector<std::pair<uintptr_t, uintptr_t>> out;
+    uintptr_t a = (uintptr_t)p;
+    const uintptr_t b = a + len;
+    std::lock_guard<std::mutex> g(g_host_mu);
+    for (const HostPiece &r : g_pieces) {
+        if (a >= b) break;
+        if (r.hi <= a) continue;
+        if (r.lo > a) return {};
+        const uintptr_t e = r.hi < b ? r.hi : b;
+        out.emplace_back(a, e);
+        a = e;
+    }
+    if (a < b) return {};
+    return out;
+}
+
+static bool host_registered(const void *p, size_t len) { return len == 0 || !host_cover(p, len).empty(); }
+
+// hipMemcpyAsync with the host side cut at piece boundaries
+static hipError_t copy_pinned(void *dst, const void *src, size_t n, hipMemcpyKind kind, hipStream_t st)
+{
+    const bool h2d = kind == hipMemcpyHostToDevice;
+    const uint8_t *host = (const uint8_t *)(h2d ? src : dst);
+    const auto parts = host_cover(host, n);
+    if (parts.empty()) return hipMemcpyAsync(dst, src, n, kind, st);
+    for (const auto &pc : parts) {
+        const size_t off = pc.first - (uintptr_t)host, len = pc.second - pc.first;
+        const hipError_t e = h2d ? hipMemcpyAsync((uint8_t *)dst + off, (const uint8_t *)src + off, len, kind, st)
+                                 : hipMemcpyAsync((uint8_t *)dst + off, (const uint8_t *)src + off, len, kind, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+int qpp_host_register(void *ptr, size_t len)
+{
+    if (!ptr || !len) return QPP_E_ARG;
+    const uintptr_t lo = (uintptr_t)ptr & ~(kPage - 1), hi = ((uintptr_t)ptr + len + kPage - 1) & ~(kPage - 1);
+    // the pieces this request needs: first page, interior, last page
+    std::vector<HostPiece> want;
+    want.push_back(HostPiece{lo, lo + kPage, 0});
+    if (hi - lo > 2 * kPage) want.push_back(HostPiece{lo + kPage, hi - kPage, 0});
+    if (hi - lo > kPage) want.push_back(HostPiece{hi - kPage, hi, 0});
+    std::lock_guard<std::mutex> g(g_host_mu);
+    for (const HostReq &q : g_reqs)
+        if (q.key == (uintptr_t)ptr) return QPP_E_ARG;  // registered already
+    // each wanted piece exists as it is (a shared boundary page) or meets
+    // no piece at all; anything else overlaps another registered range
+    std::vector<bool> have(want.size(), false);
+    for (size_t i = 0; i < want.size(); ++i)
+        for (const HostPiece &r : g_pieces) {
+            if (r.hi <= want[i].lo || r.lo >= want[i].hi) continue;
+            if (r.lo == want[i].lo && r.hi == want[i].hi && want[i].hi - want[i].lo == kPage) {
+                have[i] = true;
+                continue;
+            }
+            return QPP_E_ARG;
+        }
+    for (size_t i = 0; i < want.size(); ++i) {
+        if (have[i]) continue;
+        if (hipHostRegister((void *)want[i].lo, want[i].hi - want[i].lo, hipHostRegisterPortable) != hipSuccess) {
+            (void)hipGetLastError();
+            for (size_t j = 0; j < i; ++j)
+                if (!have[j]) (void)hipHostUnregister((void *)want[j].lo);
+            (void)hipGetLastError();
+            return QPP_E_HIP;
+        }
+    }
+    for (size_t i = 0; i < want.size(); ++i)
+        if (!have[i]) g_pieces.push_back(want[i]);
+    std::sort(g_pieces.begin(), g_pieces.end(), [](const HostPiece &x, const HostPiece &y) { return x.lo < y.lo; });
+    for (HostPiece &r : g_pieces)
+        if (r.lo < hi && r.hi > lo) ++r.refs;
+    g_reqs.push_back(HostReq{(uintptr_t)ptr, lo, hi});
+    return QPP_OK;
+}
+
+int qpp_host_unregister(void *ptr)
+{
+    std::lock_guard<std::mutex> g(g_host_mu);
+    for (size_t i = 0; i < g_reqs.size(); ++i) {
+        if (g_reqs[i].key != (uintptr_t)ptr) continue;
+        const uintptr_t lo = g_reqs[i].lo, hi = g_reqs[i].hi;
+        g_reqs.erase(g_reqs.begin() + (ptrdiff_t)i);
+        int rc = QPP_OK;
+        for (size_t k = 0; k < g_pieces.size();) {
+            HostPiece &r = g_pieces[k];
+            if (r.lo < hi && r.hi > lo && --r.refs == 0) {
+                if (hipHostUnregister((void *)r.lo) != hipSuccess) {
+                    (void)hipGetLastError();
+                    rc = QPP_E_HIP;
+                }
+                g_pieces.erase(g_pieces.begin() + (ptrdiff_t)k);
+                continue;
+            }
+            ++k;
+        }
+        return rc;
+    }
+    return QPP_E_ARG;
+}
+
+// Chunk c of the batch: its descriptors are copied into pinned staging and
+// bounds-checked by the host, and they and the chunk's input extent go H2D on
+// s_in (from the caller's memory when it is registered, else after a host
+// copy into pinned staging); the chunk's kernels run on the kernel stream
+// once that lands; its output tile and results go D2H on s_out (into the
+// caller's memory when registered), and are copied out by the host while
+// later chunks are in flight.  So host copies, both PCIe directions and the
+// kernels of different chunks overlap, and no work on the whole batch
+// precedes the first chunk's copies.
 static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
                                  const qpp_desc *desc, uint32_t n, const uint8_t *in,
                                  size_t in_len, uint8_t *out, size_t out_len, qpp_result *res,
@@ -2968,9 +3190,12 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     qpp_desc *dd = (qpp_desc *)s->d_misc;
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
-    memcpy(hd, desc, (size_t)n * sizeof(qpp_desc));
-    reject_out_of_bounds(enc, hd, n, in_len, out_len);
-    HIPCHK(hipMemcpyAsync(dd, hd, (size_t)n * sizeof(qpp_desc), hipMemcpyHostToDevice, s->s_in));
+    const bool in_direct = in == s->h_in || host_registered(in, in_len);
+    const bool out_direct = out == s->h_out || host_registered(out, out_len);
+    const bool res_direct = host_registered(res, (size_t)n * sizeof(qpp_result));
+    const uint8_t *h_src = in_direct ? in : s->h_in;
+    uint8_t *h_dst = out_direct ? out : s->h_out;
+    qpp_result *h_res = res_direct ? res : hr;
     HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     size_t olo[kPipeMaxChunks + 1];
     uint32_t first[kPipeMaxChunks + 1];
@@ -2979,10 +3204,21 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         olo[c] = c == 0 ? 0 : c == chunks ? out_len : (size_t)desc[first[c]].out_off;
         if (olo[c] > out_len) olo[c] = out_len;
     }
+    // a chunk handed back to the caller: its output tile and results
+    auto hand_back = [&](int d) {
+        if (olo[d + 1] > olo[d] && !out_direct) par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d]);
+        if (!res_direct)
+            memcpy(res + first[d], hr + first[d], (size_t)(first[d + 1] - first[d]) * sizeof(qpp_result));
+    };
     int rc = QPP_OK;
     int next_out = 0;
     for (int c = 0; c < chunks; ++c) {
         const uint32_t a = first[c], b = first[c + 1];
+        memcpy(hd + a, desc + a, (size_t)(b - a) * sizeof(qpp_desc));
+        reject_out_of_bounds(enc, hd + a, b - a, in_len, out_len);
+        if (b > a)
+            HIPCHK(hipMemcpyAsync(dd + a, hd + a, (size_t)(b - a) * sizeof(qpp_desc), hipMemcpyHostToDevice,
+                                  s->s_in));
         size_t lo = SIZE_MAX, hi = 0;
         for (uint32_t i = a; i < b; ++i) {
             if (hd[i].flags & kFlagReject) continue;
@@ -2993,9 +3229,8 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         }
         if (hi > in_len) hi = in_len;
         if (lo < hi) {
-            if (in != s->h_in) par_memcpy(s->h_in + lo, in + lo, hi - lo);
-            HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice,
-                                  s->s_in));
+            if (!in_direct) par_memcpy(s->h_in + lo, in + lo, hi - lo);
+            HIPCHK(copy_pinned(s->d_in + lo, h_src + lo, hi - lo, hipMemcpyHostToDevice, s->s_in));
         }
         HIPCHK(hipEventRecord(s->ev_in[c], s->s_in));
         HIPCHK(hipStreamWaitEvent(s->stream, s->ev_in[c], 0));
@@ -3006,8 +3241,11 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         HIPCHK(hipEventRecord(s->ev_k[c], s->stream));
         HIPCHK(hipStreamWaitEvent(s->s_out, s->ev_k[c], 0));
         if (olo[c + 1] > olo[c])
-            HIPCHK(hipMemcpyAsync(s->h_out + olo[c], s->d_out + olo[c], olo[c + 1] - olo[c],
-                                  hipMemcpyDeviceToHost, s->s_out));
+            HIPCHK(copy_pinned(h_dst + olo[c], s->d_out + olo[c], olo[c + 1] - olo[c], hipMemcpyDeviceToHost,
+                               s->s_out));
+        if (b > a)
+            HIPCHK(copy_pinned(h_res + a, dr + a, (size_t)(b - a) * sizeof(qpp_result), hipMemcpyDeviceToHost,
+                               s->s_out));
         HIPCHK(hipEventRecord(s->ev_out[c], s->s_out));
         // hand back chunks whose D2H has already landed while later ones fly
         while (next_out < c) {
@@ -3015,20 +3253,15 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
                 (void)hipGetLastError();  // hipErrorNotReady must not reach a later HIPCHK
                 break;
             }
-            const int d = next_out++;
-            if (olo[d + 1] > olo[d] && out != s->h_out)
-                par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d]);
+            hand_back(next_out++);
         }
     }
     if (rc != QPP_OK) return rc;
-    HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->s_out));
     for (int c = next_out; c < chunks; ++c) {
         HIPCHK(hipEventSynchronize(s->ev_out[c]));
-        if (olo[c + 1] > olo[c] && out != s->h_out)
-            par_memcpy(out + olo[c], s->h_out + olo[c], olo[c + 1] - olo[c]);
+        hand_back(c);
     }
     HIPCHK(hipStreamSynchronize(s->s_out));
-    memcpy(res, hr, (size_t)n * sizeof(qpp_result));
     return QPP_OK;
 }
 

@@ -8,10 +8,14 @@ PACKET_MAX = 1500
 TAG_LEN = 16
 MAX_HDR = 1500
 
+# the message of a packet the engine gave up on (S_INTERNAL: a kernel's
+# bounded wait ran out; never expected)
+INTERNAL_ERROR = "Internal error: the packet was not processed"
+
 F_NO_HP = 1
 F_RFC_PN = 2
 
-S_OK, S_LENGTH, S_DECRYPT, S_KEY_PHASE, S_NO_KEY = 0, 1, 2, 3, 4
+S_OK, S_LENGTH, S_DECRYPT, S_KEY_PHASE, S_NO_KEY, S_INTERNAL = 0, 1, 2, 3, 4, 5
 
 DESC = np.dtype(
     [

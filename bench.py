@@ -126,11 +126,44 @@ _NAMES = {0: (b"aes-128-gcm", b"aes-128-ecb", 16), 1: (b"aes-256-gcm", b"aes-256
           2: (b"chacha20-poly1305", b"chacha20", 32)}
 
 
-def _cpu_loop(w, seconds: float, part: int = 0, parts: int = 1):
-    """aioquic's own per-packet path (CryptoContext.encrypt_packet =
-    AEAD.encrypt + HeaderProtection.apply; decrypt_packet = remove +
-    decode_packet_number + AEAD.decrypt, quic/crypto.py:75-116) over a bounded
-    sample of the workload's packets; returns (packets, seconds, kind)."""
+class _RefContext:
+    """The call sequence of the reference's CryptoContext.encrypt_packet /
+    decrypt_packet (quic/crypto.py:75-116) over its own AEAD / HeaderProtection
+    objects: attribute lookups, the key-phase test and the decode of
+    quic/packet.py:118-132 included (the reference's crypto.py itself cannot
+    travel to the GPU box; this restates its method bodies)."""
+
+    def __init__(self, aead, hp, key_phase=0):
+        self.aead, self.hp, self.key_phase = aead, hp, key_phase
+
+    def encrypt_packet(self, plain_header, plain_payload, packet_number):
+        protected_payload = self.aead.encrypt(plain_payload, plain_header, packet_number)
+        return self.hp.apply(plain_header, protected_payload)
+
+    def decrypt_packet(self, packet, encrypted_offset, expected_packet_number):
+        from aioquic_amd.packet import decode_packet_number
+
+        plain_header, packet_number = self.hp.remove(packet, encrypted_offset)
+        first_byte = plain_header[0]
+        pn_length = (first_byte & 0x03) + 1
+        packet_number = decode_packet_number(packet_number, pn_length * 8, expected_packet_number)
+        crypto = self
+        if not first_byte & 0x80:
+            key_phase = (first_byte & 4) >> 2
+            assert key_phase == self.key_phase  # the bench's packets never change phase
+        payload = crypto.aead.decrypt(packet[len(plain_header):], plain_header, packet_number)
+        return plain_header, payload, packet_number, crypto != self
+
+
+def _cpu_loop(w, seconds: float, part: int = 0, parts: int = 1, samples: int = 1, mode: str = "objects"):
+    """aioquic's own per-packet path over a bounded sample of the workload's
+    packets, `samples` timed slices of seconds / samples each; returns
+    (packets, seconds, kind, per-slice GiB/s).
+    mode "objects": the AEAD / HeaderProtection calls of
+    CryptoContext.encrypt_packet (AEAD.encrypt + HeaderProtection.apply) and
+    decrypt_packet (remove + decode_packet_number + AEAD.decrypt) made
+    directly; mode "context": through _RefContext, the methods' own bodies
+    (quic/crypto.py:75-116)."""
     from aioquic_amd.packet import decode_packet_number
 
     ref = _load_reference()
@@ -153,37 +186,43 @@ def _cpu_loop(w, seconds: float, part: int = 0, parts: int = 1):
         key, iv, hp = bytes(k["key"][:kl]), bytes(k["iv"]), bytes(k["hp"][:kl])
         if ref is not None:
             objs[sl] = (ref.AEAD(an, key, iv), ref.HeaderProtection(hn, hp))
+            if mode == "context":
+                objs[sl] = _RefContext(*objs[sl])
         else:
             objs[sl] = (suite, key, iv, hp)
     ko = [objs[sl] for sl in slots]
     done = 0
-    t_p = t_u = 0.0
-    t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end:
-        t0 = time.perf_counter()
-        if ref is not None:
-            wire = [o[1].apply(p[:11], o[0].encrypt(p[11:], p[:11], pn)) for p, pn, o in zip(pk, pns, ko)]
-        else:
-            wire = [orc.protect(o[0], o[1], o[2], o[3], p[:11], p[11:], pn) for p, pn, o in zip(pk, pns, ko)]
-        t1 = time.perf_counter()
-        if ref is not None:
-            for x, pn, o in zip(wire, pns, ko):
-                hdr, trunc = o[1].remove(x, 9)
-                pnd = decode_packet_number(trunc, ((hdr[0] & 3) + 1) * 8, pn)
-                o[0].decrypt(x[len(hdr):], hdr, pnd)
-        else:
-            for x, pn, o in zip(wire, pns, ko):
-                orc.unprotect(o[0], o[1], o[2], o[3], x, 9, pn)
-        t2 = time.perf_counter()
-        t_p += t1 - t0
-        t_u += t2 - t1
-        done += m
-    return done, t_p + t_u, kind
+    t_all = 0.0
+    rates = []
+    for _ in range(max(1, samples)):
+        t_end = time.perf_counter() + seconds / max(1, samples)
+        n0, t_s = done, 0.0
+        while time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            if ref is not None and mode == "context":
+                wire = [o.encrypt_packet(p[:11], p[11:], pn) for p, pn, o in zip(pk, pns, ko)]
+                for x, pn, o in zip(wire, pns, ko):
+                    o.decrypt_packet(x, 9, pn)
+            elif ref is not None:
+                wire = [o[1].apply(p[:11], o[0].encrypt(p[11:], p[:11], pn)) for p, pn, o in zip(pk, pns, ko)]
+                for x, pn, o in zip(wire, pns, ko):
+                    hdr, trunc = o[1].remove(x, 9)
+                    pnd = decode_packet_number(trunc, ((hdr[0] & 3) + 1) * 8, pn)
+                    o[0].decrypt(x[len(hdr):], hdr, pnd)
+            else:
+                wire = [orc.protect(o[0], o[1], o[2], o[3], p[:11], p[11:], pn) for p, pn, o in zip(pk, pns, ko)]
+                for x, pn, o in zip(wire, pns, ko):
+                    orc.unprotect(o[0], o[1], o[2], o[3], x, 9, pn)
+            t_s += time.perf_counter() - t0
+            done += m
+        t_all += t_s
+        rates.append((done - n0) * 1200 / t_s / GIB)
+    return done, t_all, kind, rates
 
 
 def _cpu_worker(args):
     w, seconds, part, parts = args
-    return _cpu_loop(w, seconds, part, parts)
+    return _cpu_loop(w, seconds, part, parts)[:3]
 
 
 def cpu_share() -> int:
@@ -195,13 +234,50 @@ def cpu_share() -> int:
     return max(1, min(n, 16))
 
 
-def cpu_baseline(w, seconds: float, cfg, procs: int = 1):
+def host_identity():
+    """(CPU model, OpenSSL_version() of the libcrypto the reference's _crypto
+    links) for the baseline's line."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    ssl = None
+    if _load_reference() is not None:
+        try:
+            paths = {ln.split()[-1] for ln in open("/proc/self/maps") if "libcrypto" in ln}
+            for path in sorted(paths):
+                lib = ctypes.CDLL(path)
+                lib.OpenSSL_version.restype = ctypes.c_char_p
+                lib.OpenSSL_version.argtypes = [ctypes.c_int]
+                ssl = {"version": lib.OpenSSL_version(0).decode(), "path": path}
+                break
+        except (OSError, AttributeError):
+            pass
+    return model, ssl
+
+
+def cpu_baseline(w, seconds: float, cfg, procs: int = 1, samples: int = 5):
     """The reference's CPU path timed on `procs` host cores (one process per
     core, each with its own AEAD/HP objects and packets, like one aioquic
-    connection per core).  Runs BEFORE the GPU is initialised (fork)."""
+    connection per core).  Runs BEFORE the GPU is initialised (fork).  On one
+    core: the median of `samples` slices of the objects-only sequence, then
+    the same through the CryptoContext method bodies."""
+    extra = {}
     if procs <= 1:
-        done, t, kind = _cpu_loop(w, seconds)
-        value = done * 1200 / t / GIB
+        half = seconds / 2
+        done, t, kind, rates = _cpu_loop(w, half, samples=samples)
+        value = float(np.median(rates))
+        if kind == "reference":
+            _, _, _, crates = _cpu_loop(w, half, samples=samples, mode="context")
+            extra = {"samples_gib_s": [round(r, 4) for r in rates], "median_of": len(rates),
+                     "context_value": round(float(np.median(crates)), 4),
+                     "context_samples_gib_s": [round(r, 4) for r in crates]}
+        else:
+            extra = {"samples_gib_s": [round(r, 4) for r in rates], "median_of": len(rates)}
     else:
         import multiprocessing as mp
 
@@ -210,11 +286,19 @@ def cpu_baseline(w, seconds: float, cfg, procs: int = 1):
         done = sum(r[0] for r in res)
         kind = res[0][2]
         value = sum(r[0] * 1200 / r[1] for r in res) / GIB
+    model, ssl = host_identity()
     an = "/".join(sorted({_NAMES[int(s)][0].decode() for s in w.suites[: min(w.n, 20000)]}))
-    return {"value": round(value, 4), "unit": "GiB/s", "cores": procs, "kind": kind,
-            "sample": f"{done} packets of the bench workload ({cfg['name']}), suites {an}, "
-                      f"per-packet {'aioquic _crypto.c + OpenSSL' if kind == 'reference' else 'C oracle'}"
-                      f" calls, ~{seconds:.0f} s on {procs} core(s) of the GPU host"}
+    what = ("AEAD/HP objects only: AEAD.encrypt + HeaderProtection.apply, then remove + decode_packet_number + "
+            "AEAD.decrypt per packet, no CryptoContext wrapper (context_value: through the bodies of "
+            "CryptoContext.encrypt_packet/decrypt_packet, quic/crypto.py:75-116)"
+            if kind == "reference" else "C oracle protect/unprotect per packet")
+    out = {"value": round(value, 4), "unit": "GiB/s", "cores": procs, "kind": kind,
+           "sample": f"{done} packets of the bench workload ({cfg['name']}), suites {an}; {what}; "
+                     f"~{seconds:.0f} s on {procs} core(s) of the GPU host"
+                     + (f", median of {samples} slices" if procs <= 1 else ", one slice per core, summed"),
+           "cpu_model": model, "libcrypto": ssl}
+    out.update(extra)
+    return out
 
 
 # --------------------------------------------------------------------- main --
@@ -480,9 +564,11 @@ def main():
     torch.cuda.synchronize(dev)
 
     # the timed region: K steps on one stream; in every `--event-every`-th step
-    # each kernel sits between two timing-only HIP events (its launch duration
-    # for the roofline).  Sampling keeps the events' own stream time (a few us
-    # per record) out of most steps of `value`.
+    # (by default every step, since round 4) each kernel sits between two
+    # timing-only HIP events (its launch duration for the roofline).  The
+    # records' own stream time (~6 us per step: 0.25 % of a north-star step,
+    # ~3 % of config 2's) is inside `value`; --event-every 10 keeps it out of
+    # 9 steps in 10, as rounds 1-3 measured.
     every = max(1, args.event_every)
     # (sampled: not the first timed step, which follows the barrier, the
     # others follow a step)
@@ -622,35 +708,56 @@ def e2e_host_devices(cfg, seed, n, reps=3):
     (MultiDeviceEngine / qpp_multi: one host batch cut into contiguous ranges,
     one session and key-table replica per device, host threads in parallel):
     host memory -> protect -> host, then host -> unprotect -> host, per device
-    count 1..D.  PCIe-inclusive; never the bench value."""
+    count 1..D, with the caller's arrays registered (qpp_host_register: DMA
+    straight from / to them, `gib_s`) and as plain pageable arrays (copied
+    through the session's pinned staging, `staged_gib_s`).  PCIe-inclusive;
+    never the bench value."""
     import torch
-    from aioquic_amd.batch import MultiDeviceEngine
+    from aioquic_amd.batch import MultiDeviceEngine, register_host
     from aioquic_amd.bench_data import make_workload
 
     w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=seed, version=cfg["version"],
                       mixed=cfg.get("mixed"))
     out = {}
+    plain = np.ascontiguousarray(w.plain)
     wire = np.empty(w.wire_size, np.uint8)
     back = np.empty(w.plain_size, np.uint8)
     r1 = np.empty(n, L_RESULT())
     r2 = np.empty(n, L_RESULT())
-    for d in range(1, torch.cuda.device_count() + 1):
-        eng = MultiDeviceEngine(w.n_keys, devices=list(range(d)))
-        eng.set_key_records(w.keys)
-        eng.protect_into(w.desc, w.plain, wire, r1)  # warm-up (staging allocation, first touch)
+
+    def run(eng):
+        eng.protect_into(w.desc, plain, wire, r1)  # warm-up (staging allocation, first touch)
         eng.unprotect_into(w.udesc, wire, back, r2)
         times = []
         for _ in range(reps):
+            back[:1] ^= 1  # the round trip below must rewrite it
             t0 = time.perf_counter()
-            eng.protect_into(w.desc, w.plain, wire, r1)
+            eng.protect_into(w.desc, plain, wire, r1)
             eng.unprotect_into(w.udesc, wire, back, r2)
             times.append(time.perf_counter() - t0)
-        ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all() and np.array_equal(back, w.plain))
-        out[str(d)] = {"gib_s": round(n * 1200 / float(np.median(times)) / GIB, 3), "round_trip_ok": ok}
+        ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all() and np.array_equal(back, plain))
+        return round(n * 1200 / float(np.median(times)) / GIB, 3), ok
+
+    for d in range(1, torch.cuda.device_count() + 1):
+        eng = MultiDeviceEngine(w.n_keys, devices=list(range(d)))
+        eng.set_key_records(w.keys)
+        staged, ok_s = run(eng)
+        t0 = time.perf_counter()
+        regs = register_host(plain, wire, back, r1, r2)
+        reg_ms = (time.perf_counter() - t0) * 1e3
+        try:
+            direct, ok_d = run(eng)
+        finally:
+            for r in regs:
+                r.close()
+        out[str(d)] = {"gib_s": direct, "round_trip_ok": ok_d and ok_s, "staged_gib_s": staged,
+                       "register_ms": round(reg_ms, 1)}
         del eng
     return {"per_device_count": out, "packets": n,
             "note": "caller-owned host arrays: qpp_multi protect_into, then unprotect_into (two synchronous "
-                    "calls, each staged through pinned memory, H2D, kernel, D2H)"}
+                    "calls; each a chunked H2D / kernel / D2H pipeline). gib_s: the arrays registered once "
+                    "(qpp_host_register, register_ms; DMA straight from / to them); staged_gib_s: pageable "
+                    "arrays copied through pinned staging by host threads"}
 
 
 def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5, mode="staged"):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define QPP_ABI_VERSION 3
+#define QPP_ABI_VERSION 4
 
 /* cipher suites (quic/crypto.py:12-16 CIPHER_SUITES) */
 #define QPP_AES_128_GCM 0        /* aes-128-gcm + aes-128-ecb header protection */
@@ -67,6 +67,11 @@ extern "C" {
 #define QPP_S_KEY_PHASE 3   /* short header whose key-phase bit differs from the slot's
                                (quic/crypto.py:91-96): caller retries with the next-phase key */
 #define QPP_S_NO_KEY 4      /* slot never installed: KeyUnavailableError (quic/crypto.py:78-79) */
+#define QPP_S_INTERNAL 5    /* the engine gave up on the packet: a bounded wait inside a kernel
+                               (a GHASH table entry, a two-wave hand-over) ran out.  Nothing at
+                               out_off is valid (unprotect: no plaintext is left there), and the
+                               call raises CryptoError, as a failed reference call does
+                               (_crypto.c:17-29).  Never expected; counted by qpp_watchdog_count */
 
 /* descriptor flags */
 #define QPP_F_NO_HP 1u      /* AEAD only (AEAD.encrypt/.decrypt): no header protection, no
@@ -135,9 +140,10 @@ int qpp_abi_version(void);
 /* 16 hex digits: the hash of the native sources the library was built from
  * (aioquic_amd/_srchash.py); a binding checks it against its own at load. */
 const char *qpp_source_hash(void);
-/* GCM table-entry watchdog events on the current device since the library
- * loaded: a launch whose kernel waited ~1 s for a GHASH table entry skipped
- * that key slot's packets without writing their results.  Never expected
+/* Watchdog events on the current device since the library loaded: a launch
+ * whose kernel waited ~1 s for a GHASH table entry (that key slot's packets),
+ * or a two-wave packet whose hand-over timed out, reported QPP_S_INTERNAL
+ * for the packets concerned.  Never expected
  * (it would be a bug); tests check it stays 0.  A synchronous read. */
 uint32_t qpp_watchdog_count(void);
 const char *qpp_strerror(int rc);
@@ -225,6 +231,21 @@ int qpp_session_hp_mask(qpp_session *s, const qpp_keytab *kt, const uint32_t *sl
 int qpp_session_stage(qpp_session *s, size_t bytes, uint32_t n, uint8_t **h_in, uint8_t **h_out);
 int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material *km,
                          uint32_t n);
+
+/* Registered host buffers (ABI 4).  A server's socket buffers are long-lived
+ * (the datagrams of src/aioquic/asyncio/protocol.py:121-122,154-158 arrive in
+ * and leave from them), so a caller may pin them once: qpp_host_register
+ * page-locks [ptr, ptr + len) for every device (hipHostRegister, portable).
+ * A session call whose input, output or result array lies inside a registered
+ * range moves it by DMA straight from / to the caller's memory instead of
+ * copying it through the session's pinned staging (the bytes written are the
+ * same).  Two ranges may share a boundary page (pinned once, reference-
+ * counted); a range that overlaps a registered one otherwise, or the same ptr
+ * twice, is refused (QPP_E_ARG) -- a sub-range of a registered array needs
+ * no registration of its own.  The range must stay allocated until
+ * qpp_host_unregister(ptr) with the same ptr.  Thread-safe. */
+int qpp_host_register(void *ptr, size_t len);
+int qpp_host_unregister(void *ptr);
 
 /* One host batch over several GPUs of the node (the
  * server socket of src/aioquic/asyncio/server.py:60-152 feeds all

@@ -162,8 +162,9 @@ def test_wave_items_ragged_runs(oracle, plan_path):
 def _full_size(cfg, n, n_keys, seed, oracle):
     """Full-size random-arrival batch on device tensors, bucketed in the
     product: every tag verifies, the round trip is exact, decoded packet
-    numbers are the sent ones, and for every key its first packet equals the
-    oracle byte for byte."""
+    numbers are the sent ones, and every packet in both directions equals the
+    reference's own _crypto byte for byte (the C oracle on the first packet of
+    every key when oracle/_ref is not built)."""
     import torch
 
     from aioquic_amd import bench_data
@@ -190,13 +191,27 @@ def _full_size(cfg, n, n_keys, seed, oracle):
     assert (r2["status"] == 0).all()
     assert (r2["pn"] == w.desc["pn"]).all()
     assert torch.equal(d_back, d_in)
-    # the first packet of every key against the oracle
+    wire = d_wire.cpu().numpy()
+    back = d_back.cpu().numpy()
+    # whole-batch parity: every packet in both directions
+    # against the reference's own _crypto (oracle/_ref: _crypto.c:115-194
+    # driven as quic/crypto.py:75-116 drives it) when it is built; otherwise
+    # the first packet of every key against the C oracle
+    from tests import ref_crypto
+
+    ref = ref_crypto.load()
+    if ref is not None:
+        assert np.array_equal(ref_crypto.protect_all(ref, w), wire)
+        r_back, r_pn = ref_crypto.unprotect_all(ref, w, wire)
+        assert np.array_equal(r_back, back)
+        assert np.array_equal(r_pn, r2["pn"])
+        return w
     _, first = np.unique(w.desc["slot"], return_index=True)
     assert len(first) == n_keys
     sub = w.desc[first].copy()
     o_out, o_res = oracle.protect_batch(w.keys, sub, w.plain, w.wire_size)
     assert (o_res["status"] == 0).all()
-    wire_rows = d_wire.view(n, 1200)[torch.from_numpy(first.astype(np.int64)).cuda()].cpu().numpy()
+    wire_rows = wire.reshape(n, 1200)[first]
     want_rows = o_out.reshape(n, 1200)[first]
     assert np.array_equal(wire_rows, want_rows)
     return w

@@ -24,21 +24,21 @@ def L():
     return layout
 
 
-def _chunks(n, rng):
-    """Chunk sizes 1..16 covering n packets (the lone kernels' launch sizes)."""
+def _chunks(n, rng, chunk=CHUNK):
+    """Chunk sizes 1..chunk covering n packets (the lone kernels' launch sizes)."""
     out, i = [], 0
     while i < n:
-        k = int(rng.integers(1, CHUNK + 1))
+        k = int(rng.integers(1, chunk + 1))
         out.append(slice(i, min(n, i + k)))
         i += k
     return out
 
 
-def _check_round_trip(oracle, L, eng, recs, headers, payloads, pns, slots, rng, flags=0):
+def _check_round_trip(oracle, L, eng, recs, headers, payloads, pns, slots, rng, flags=0, chunk=CHUNK):
     from aioquic_amd.batch import layout_packets
 
     n_ok = 0
-    for sl in _chunks(len(headers), rng):
+    for sl in _chunks(len(headers), rng, chunk):
         h, p, pn, s = headers[sl], payloads[sl], pns[sl], slots[sl]
         inbuf, desc, size = layout_packets(h, p, pn, s, flags=flags)
         out_g, res_g = eng.protect_host(desc, inbuf.tobytes(), size)
@@ -109,6 +109,43 @@ def test_lone_aead_only_long_aad(oracle, L, suite):
     pns = [int(rng.integers(0, 1 << 62)) for _ in sizes]
     slots = [i % 2 for i in range(len(sizes))]
     _check_round_trip(oracle, L, eng, recs, aads, datas, pns, slots, rng, flags=L.F_NO_HP)
+
+
+@pytest.mark.parametrize("suite", [0, 1, 2])
+def test_lone_long_header_hp(oracle, L, suite):
+    """Header protection with long headers (1000-1480 B, up to QPP_MAX_HDR
+    with the packet's 1500-byte limit) and short payloads (clen < 20 and
+    < 32: the sample then overlaps the tag), in launches of 1-8 packets (pair
+    launches: for AES-GCM the header is past the first wave's 64 positions,
+    so CT blocks 0-1 come from the second wave through LDS), both
+    directions, against the oracle."""
+    from aioquic_amd.batch import PacketEngine
+
+    rng = np.random.default_rng(0x10A6 + suite)
+    recs = _keys(rng, 3, (suite,))
+    eng = PacketEngine(3)
+    eng.set_key_records(recs)
+    headers, payloads, pns, slots = [], [], [], []
+    for i in range(96):
+        pn_len = 1 + i % 4
+        pn = int(rng.integers(0, 1 << 30))
+        hlen = int(rng.choice([1000, 1008, 1023, 1024, 1200, 1399, 1400, 1450, 1479]))
+        clen = int(rng.choice([4 - pn_len, 3, 7, 15, 16, 17, 19, 20, 24, 31, 32, 33, 40]))
+        clen = max(4 - pn_len, min(clen, 1500 - 16 - hlen))
+        # an Initial whose token pads the header to hlen
+        fixed = 1 + 4 + 1 + 8 + 1 + 2 + 2 + pn_len
+        tok = hlen - fixed
+        hdr = (bytes([0xC0 | (pn_len - 1)]) + (1).to_bytes(4, "big") + b"\x08" + rng.bytes(8) + b"\x00" +
+               bytes([0x40 | (tok >> 8), tok & 0xFF]) + rng.bytes(tok) + bytes([0x40 | ((clen + pn_len + 16) >> 8),
+                                                                                    (clen + pn_len + 16) & 0xFF]) +
+               (pn & ((1 << (8 * pn_len)) - 1)).to_bytes(pn_len, "big"))
+        assert len(hdr) == hlen
+        headers.append(hdr)
+        payloads.append(rng.bytes(clen))
+        pns.append(pn)
+        slots.append(i % 3)
+    n_ok = _check_round_trip(oracle, L, eng, recs, headers, payloads, pns, slots, rng, chunk=8)
+    assert n_ok > 60
 
 
 def test_lone_status_paths(oracle, L):

@@ -385,3 +385,17 @@ def test_key_release_from_another_thread_is_queued():
     assert len(slots._keep) == 1 and slots._inbox  # queued (recv and send), not applied
     slots.assign([])
     assert len(slots._keep) == 0 and not slots._inbox and not slots._by_obj
+    # an owner that stops assigning: close() applies the queue and frees the rest
+    p2, q = CryptoPair(), CryptoPair()
+    p2.setup_initial(bytes(8), is_client=True, version=QuicProtocolVersion.VERSION_1)
+    q.setup_initial(bytes(8), is_client=False, version=QuicProtocolVersion.VERSION_1)
+    sb.add(p2, bytes([0x41]) + bytes(8) + bytes(2), bytes(40), 1)
+    sb.add(q, bytes([0x41]) + bytes(8) + bytes(2), bytes(40), 0)
+    sb.flush()
+    assert len(slots._keep) == 2
+    t = threading.Thread(target=q.teardown)
+    t.start()
+    t.join()
+    assert slots._inbox
+    slots.close()
+    assert len(slots._keep) == 0 and not slots._inbox and not slots._by_obj and not slots._slot
