@@ -93,10 +93,19 @@ constexpr int kGh5Hi = 27 * 256;  // offset of the high halves
 constexpr int kGh5Bytes = 14 * 1024;
 constexpr int kGh5Off = kGhashPowers * kGhashPowBytes;  // offset of the 5-bit H^4 in a slot's tables
 // H^1 .. H^kGhPowCount as plain 16-byte elements, for the lone-packet kernel
-// (k_lone: GHASH as sum_i X_i H^(m-i) over a packet's m <= 189 blocks)
+// (k_lone: GHASH as sum_i X_i H^(m-i) over a packet's m <= 189 blocks), in
+// their own region after every slot's tables (gh_powers), so the slot stride
+// of the quad kernels' tables stays 46 KiB (round 5).
 constexpr int kGhPowCount = 192;
-constexpr int kGhPowOff = kGh5Off + kGh5Bytes;
-constexpr int kGhashTabBytes = kGhPowOff + kGhPowCount * 16;  // 49 KiB per slot
+constexpr int kGhPowBytes = kGhPowCount * 16;
+constexpr int kGhashTabBytes = kGh5Off + kGh5Bytes;  // 46 KiB per slot
+// byte offset of slot's H^1.. in a table of `cap` slots (round 4 kept them
+// inside each slot's tables at a 49 KiB stride: config 4 measured the same
+// either way, same box interleaved, profiles/r5c_config4_powers_ab.txt)
+__device__ __host__ __forceinline__ size_t gh_powers_off(uint32_t cap, uint32_t slot)
+{
+    return (size_t)cap * kGhashTabBytes + (size_t)slot * kGhPowBytes;
+}
 // one LDS table entry of the GCM kernel: H^4 in the step loop's layout
 constexpr int kGhLdsEntry = kGh5Bytes;
 

@@ -1832,7 +1832,7 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         const int rlen = hlen + clen + (ENC ? 0 : QPP_TAG_LEN);
         const uint8_t *src = P.src;
         uint8_t *dst = P.dst;
-        const uint8_t *hpw = gtab + (size_t)d.slot * kGhashTabBytes + kGhPowOff;
+        const uint8_t *hpw = gtab + gh_powers_off(cap, d.slot);
         const bool masked = !ENC && P.hp;
         // a position's input block (AAD or CT; zero otherwise), its power of H
         auto input = [&](int pos) -> u32x4 {
@@ -2266,7 +2266,7 @@ __global__ __launch_bounds__(kSetupWG) void k_key_setup(KeySlot *__restrict__ sl
             if (t < have && have + t < kGhPowCount) hall[have + t] = gf128_mul_slow(hall[t], hall[have - 1]);
             __syncthreads();
         }
-        u32x4 *hp = (u32x4 *)(gtab + (size_t)m.slot * kGhashTabBytes + kGhPowOff);
+        u32x4 *hp = (u32x4 *)(gtab + gh_powers_off(cap, m.slot));
         for (int i = threadIdx.x; i < kGhPowCount; i += kSetupWG) hp[i] = hall[i];
         u32x4 *tab = (u32x4 *)(gtab + (size_t)m.slot * kGhashTabBytes);
         for (int e = threadIdx.x; e < kGhashPowers * 32 * 16; e += kSetupWG) {
@@ -2354,6 +2354,8 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -2478,7 +2480,7 @@ int qpp_keytab_create(uint32_t capacity, qpp_keytab **out)
     }
     memset(kt->h_suite, 0xff, capacity);
     if (hipMalloc(&kt->d_slots, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
-        hipMalloc(&kt->d_gtab, (size_t)capacity * kGhashTabBytes) != hipSuccess ||
+        hipMalloc(&kt->d_gtab, (size_t)capacity * (kGhashTabBytes + kGhPowBytes)) != hipSuccess ||
         hipMemset(kt->d_slots, 0xff, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
         (void)hipGetLastError();
@@ -2980,33 +2982,104 @@ void *qpp_session_stream(qpp_session *s) { return s ? (void *)s->stream : NULL; 
 // Each chunk's H2D covers the input extent of its own packets (over-copying
 // bytes of a neighbour is harmless: same host bytes).
 // Host copies between caller memory and pinned staging: one thread streams
-// ~10 GB/s, well under the PCIe rate, so large copies are split over threads.
-static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
-{
-    constexpr size_t kPart = (size_t)4 << 20;
-    constexpr int kMaxThreads = 16;
-    static const int max_threads = [] {
+// ~10 GB/s, well under the PCIe rate, so large copies are split over a
+// process-wide pool of copy threads (started on first use, never torn down:
+// its threads sleep on a condition variable between copies).  Round 5: the
+// pool replaces a std::thread per part and copy (up to 8 x 64 thread starts
+// per 1 Mi-packet call), and a chunk's copy-out runs on it while the calling
+// thread stages the next chunks.
+struct CopyGroup {
+    std::mutex mu;
+    std::condition_variable cv;
+    int pending = 0;
+    void wait()
+    {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return pending == 0; });
+    }
+};
+
+class CopyPool {
+  public:
+    static CopyPool &get()
+    {
+        static CopyPool *p = new CopyPool();  // never destroyed: no join at exit
+        return *p;
+    }
+    int threads() const { return n_; }
+    void submit(uint8_t *dst, const uint8_t *src, size_t len, CopyGroup *g)
+    {
+        {
+            std::lock_guard<std::mutex> l(g->mu);
+            ++g->pending;
+        }
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            q_.push_back(Task{dst, src, len, g});
+        }
+        cv_.notify_one();
+    }
+
+  private:
+    struct Task {
+        uint8_t *dst;
+        const uint8_t *src;
+        size_t len;
+        CopyGroup *g;
+    };
+    CopyPool()
+    {
         const char *v = getenv("QPP_COPY_THREADS");  // A/B switch, default 8
         const int t = v ? atoi(v) : 8;
-        return t < 1 ? 1 : t > kMaxThreads ? kMaxThreads : t;
-    }();
-    int parts = (int)(bytes / kPart);
-    if (parts > max_threads) parts = max_threads;
-    if (parts < 2) {
+        n_ = t < 1 ? 1 : t > 32 ? 32 : t;
+        for (int i = 0; i < n_; ++i) std::thread([this] { run(); }).detach();
+    }
+    void run()
+    {
+        for (;;) {
+            Task t;
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [&] { return !q_.empty(); });
+                t = q_.front();
+                q_.pop_front();
+            }
+            memcpy(t.dst, t.src, t.len);
+            bool last;
+            {
+                std::lock_guard<std::mutex> l(t.g->mu);
+                last = --t.g->pending == 0;
+            }
+            if (last) t.g->cv.notify_all();
+        }
+    }
+    int n_ = 8;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Task> q_;
+};
+
+// dst <- src over the pool's threads in parts of >= 4 MiB; with g, return at
+// once (g->wait() before the bytes are used), else when the copy is done.
+static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, CopyGroup *g = nullptr)
+{
+    constexpr size_t kPart = (size_t)4 << 20;
+    if (bytes < 2 * kPart) {
         memcpy(dst, src, bytes);
         return;
     }
-    std::thread th[kMaxThreads];
+    CopyPool &pool = CopyPool::get();
+    size_t parts = bytes / kPart;
+    if (parts > (size_t)pool.threads()) parts = (size_t)pool.threads();
     const size_t step = (bytes / parts + 63) & ~(size_t)63;
-    for (int t = 1; t < parts; ++t) {
-        const size_t lo = step * t;
-        if (lo >= bytes) break;
-        const size_t len = lo + step < bytes && t + 1 < parts ? step : bytes - lo;
-        th[t] = std::thread([=] { memcpy(dst + lo, src + lo, len); });
+    CopyGroup local;
+    CopyGroup *grp = g ? g : &local;
+    for (size_t lo = g ? 0 : step; lo < bytes; lo += step)
+        pool.submit(dst + lo, src + lo, lo + step < bytes ? step : bytes - lo, grp);
+    if (!g) {
+        memcpy(dst, src, step < bytes ? step : bytes);  // the caller's own part
+        local.wait();
     }
-    memcpy(dst, src, step < bytes ? step : bytes);
-    for (int t = 1; t < parts; ++t)
-        if (th[t].joinable()) th[t].join();
 }
 
 // Descriptor extents against the caller's buffer sizes (quic_pp.h, Buffers):
@@ -3204,9 +3277,16 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         olo[c] = c == 0 ? 0 : c == chunks ? out_len : (size_t)desc[first[c]].out_off;
         if (olo[c] > out_len) olo[c] = out_len;
     }
-    // a chunk handed back to the caller: its output tile and results
+    // a chunk handed back to the caller: its output tile and results, copied
+    // out by the pool while this thread goes on staging later chunks
+    CopyGroup outg;
+    struct WaitAll {
+        CopyGroup &g;
+        ~WaitAll() { g.wait(); }  // every return path: no pool copy outlives the call
+    } wait_all{outg};
     auto hand_back = [&](int d) {
-        if (olo[d + 1] > olo[d] && !out_direct) par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d]);
+        if (olo[d + 1] > olo[d] && !out_direct)
+            par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d], &outg);
         if (!res_direct)
             memcpy(res + first[d], hr + first[d], (size_t)(first[d + 1] - first[d]) * sizeof(qpp_result));
     };

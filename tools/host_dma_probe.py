@@ -64,35 +64,40 @@ pa, pb = vp(), vp()
 assert hip.hipHostMalloc(ctypes.byref(pa), N, 0) == 0 and hip.hipHostMalloc(ctypes.byref(pb), N, 0) == 0
 ctypes.memset(pa, 1, N)
 out["hipHostMalloc"] = legs(pa.value, pb.value)
-# numpy, registered
-a = np.ones(N, np.uint8)
-b = np.zeros(N, np.uint8)
-_crypto.host_register(a.ctypes.data, N)
-_crypto.host_register(b.ctypes.data, N)
-out["numpy_registered"] = legs(a.ctypes.data, b.ctypes.data)
-_crypto.host_unregister(a.ctypes.data)
-_crypto.host_unregister(b.ctypes.data)
-out["numpy_pageable"] = legs(a.ctypes.data, b.ctypes.data)
-del a, b
-# 2 MiB-aligned anonymous mmap with MADV_HUGEPAGE, registered
-maps = []
-for _ in range(2):
+hip.hipHostRegister.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint]
+hip.hipHostUnregister.argtypes = [vp]
+
+
+def anon(huge):
+    """An N-byte 2 MiB-aligned anonymous mapping (MADV_HUGEPAGE when huge)."""
     m = mmap.mmap(-1, N + (2 << 20))
-    try:
-        m.madvise(mmap.MADV_HUGEPAGE)
-    except (AttributeError, OSError):
-        pass
+    if huge:
+        try:
+            m.madvise(mmap.MADV_HUGEPAGE)
+        except (AttributeError, OSError):
+            pass
     arr = np.frombuffer(m, np.uint8)
-    base = arr.ctypes.data
-    off = (-base) % (2 << 20)
+    off = (-arr.ctypes.data) % (2 << 20)
     arr = arr[off : off + N]
     arr[:] = 1
-    maps.append((m, arr))
-_crypto.host_register(maps[0][1].ctypes.data, N)
-_crypto.host_register(maps[1][1].ctypes.data, N)
-out["mmap_hugepage_registered"] = legs(maps[0][1].ctypes.data, maps[1][1].ctypes.data)
-_crypto.host_unregister(maps[0][1].ctypes.data)
-_crypto.host_unregister(maps[1][1].ctypes.data)
+    return m, arr
+
+
+# one hipHostRegister per buffer (the copies stay inside it), by flags
+for name, huge, flags in (("registered_default", False, 0), ("registered_coarse", False, 0x8),
+                          ("registered_portable", False, 0x1), ("hugepage_registered_coarse", True, 0x8),
+                          ("hugepage_registered_default", True, 0)):
+    bufs = [anon(huge), anon(huge)]
+    ok = all(hip.hipHostRegister(b[1].ctypes.data, N, flags) == 0 for b in bufs)
+    out[name] = legs(bufs[0][1].ctypes.data, bufs[1][1].ctypes.data) if ok else "register failed"
+    for b in bufs:
+        hip.hipHostUnregister(b[1].ctypes.data)
+    del bufs
+# pageable (unregistered) numpy memory
+a = np.ones(N, np.uint8)
+b = np.zeros(N, np.uint8)
+out["numpy_pageable"] = legs(a.ctypes.data, b.ctypes.data)
+del a, b
 try:
     out["thp"] = open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()
 except OSError:
