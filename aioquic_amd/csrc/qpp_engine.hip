@@ -1315,6 +1315,20 @@ __device__ __forceinline__ void tab_release(GcmSmem<WG> &sm, uint32_t e)
     if (lane_fresh() == 0) atomicSub(&sm.eref[e], 1u);
 }
 
+// Study build only (-DQPP_STUDY_SYNTH, tools/build_variant.py): the north
+// star's descriptors and header byte 0 synthesized from the packet index
+// instead of loaded, to bound what prefetching them could gain (round 5,
+// VERDICT r4 item 3).  Wrong output by design: timing only.
+#ifdef QPP_STUDY_SYNTH
+__device__ __forceinline__ qpp_desc study_desc(const qpp_desc *, uint32_t p)
+{
+    return qpp_desc{1200ull * p, 1200ull * p, 1173u, 11, 0, (uint64_t)p, 0u, p};
+}
+#define QPP_DESC(i) study_desc(desc, (i))
+#else
+#define QPP_DESC(i) desc[i]
+#endif
+
 template <int SUITE, bool ENC, int WG, int BPL>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_gcm(const KeySlot *__restrict__ slots,
                                               const uint8_t *__restrict__ gtab, uint32_t cap,
@@ -1394,7 +1408,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             const uint32_t t = tid_now(), p = pkt_of(t);
             uint64_t in0 = ~0ull, out0 = ~0ull;
             if (p < we) {
-                const qpp_desc d = desc[p];
+                const qpp_desc d = QPP_DESC(p);
                 in0 = d.in_off;
                 out0 = d.out_off;
                 if (d.slot >= cap && (t & 3) == 0) res[planned ? d.rsv : p] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
@@ -1407,9 +1421,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         auto run_slot = [&](uint32_t cur) {
             const KeySlot *ks = slots + cur;
             const uint32_t t1 = tid_now(), p1 = pkt_of(t1);
-            const qpp_desc d = p1 < we ? desc[p1] : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
+            const qpp_desc d = p1 < we ? QPP_DESC(p1) : qpp_desc{0, 0, 0, 0, 0, 0, kNoSlot, 0};
             if (slot_of(d, p1) != cur) return;  // the lambda's only early exit, at its top
+#ifdef QPP_STUDY_SYNTH
+            const HdrPre pre = {{0x41u, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, 0x41u};
+#else
             const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
+#endif
             const LdsTe T{sm.te, (t1 & 31) * 4};
             Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
             if (P.status == QPP_S_OK) {
@@ -1436,7 +1454,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
                     const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
-                    const qpp_desc d2 = desc[p2];
+                    const qpp_desc d2 = QPP_DESC(p2);
                     Pkt Q;
                     Q.src = gin + d2.in_off;
                     Q.dst = gout + d2.out_off;
@@ -1459,7 +1477,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 }
             }
             const uint32_t t3 = tid_now(), p3 = pkt_of(t3);
-            write_result<ENC>(res, planned ? desc[p3].rsv : p3, t3 & 3, P);
+            write_result<ENC>(res, planned ? QPP_DESC(p3).rsv : p3, t3 & 3, P);
             QPP_PROBE_AT(7);
         };
 
@@ -1470,7 +1488,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll 1
         for (int guard = 0; guard < 17; ++guard) {
             const uint32_t t = tid_now(), p = pkt_of(t);
-            const uint32_t s = p < we ? slot_of(desc[p], p) : kNoSlot;
+            const uint32_t s = p < we ? slot_of(QPP_DESC(p), p) : kNoSlot;
             const uint32_t cur = wave_min_u32((last == kNoSlot || s > last) ? s : kNoSlot);
             if (cur == kNoSlot) break;
             last = cur;
@@ -2354,6 +2372,7 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -3161,7 +3180,11 @@ static std::vector<std::pair<uintptr_t, uintptr_t>> host_cover(const void *p, si
 
 static bool host_registered(const void *p, size_t len) { return len == 0 || !host_cover(p, len).empty(); }
 
-// hipMemcpyAsync with the host side cut at piece boundaries
+// hipMemcpyAsync with the host side cut at piece boundaries (registered
+// caller memory).  D2H is left to the runtime, which moves it by a blit
+// kernel beside the copy engines' H2D (forcing the copy engines with
+// DeviceToDeviceNoCU measured slower on the pipeline: both directions then
+// share them, profiles/r5g_d2h_engines.txt).
 static hipError_t copy_pinned(void *dst, const void *src, size_t n, hipMemcpyKind kind, hipStream_t st)
 {
     const bool h2d = kind == hipMemcpyHostToDevice;
@@ -3170,8 +3193,7 @@ static hipError_t copy_pinned(void *dst, const void *src, size_t n, hipMemcpyKin
     if (parts.empty()) return hipMemcpyAsync(dst, src, n, kind, st);
     for (const auto &pc : parts) {
         const size_t off = pc.first - (uintptr_t)host, len = pc.second - pc.first;
-        const hipError_t e = h2d ? hipMemcpyAsync((uint8_t *)dst + off, (const uint8_t *)src + off, len, kind, st)
-                                 : hipMemcpyAsync((uint8_t *)dst + off, (const uint8_t *)src + off, len, kind, st);
+        const hipError_t e = hipMemcpyAsync((uint8_t *)dst + off, (const uint8_t *)src + off, len, kind, st);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -3203,7 +3225,11 @@ int qpp_host_register(void *ptr, size_t len)
         }
     for (size_t i = 0; i < want.size(); ++i) {
         if (have[i]) continue;
-        if (hipHostRegister((void *)want[i].lo, want[i].hi - want[i].lo, hipHostRegisterPortable) != hipSuccess) {
+        static const unsigned reg_flags = [] {
+            const char *v = getenv("QPP_REG_FLAGS");  // study switch (round 5)
+            return v ? (unsigned)strtoul(v, nullptr, 0) : (unsigned)hipHostRegisterPortable;
+        }();
+        if (hipHostRegister((void *)want[i].lo, want[i].hi - want[i].lo, reg_flags) != hipSuccess) {
             (void)hipGetLastError();
             for (size_t j = 0; j < i; ++j)
                 if (!have[j]) (void)hipHostUnregister((void *)want[j].lo);
@@ -3245,6 +3271,19 @@ int qpp_host_unregister(void *ptr)
     return QPP_E_ARG;
 }
 
+// QPP_SESSION_TRACE=1: one stderr line per pipelined call with its host
+// phases (a study switch, read once per process)
+static bool trace_on()
+{
+    static const bool b = getenv("QPP_SESSION_TRACE") != nullptr;
+    return b;
+}
+static double trace_now()
+{
+    if (!trace_on()) return 0.0;
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // Chunk c of the batch: its descriptors are copied into pinned staging and
 // bounds-checked by the host, and they and the chunk's input extent go H2D on
 // s_in (from the caller's memory when it is registered, else after a host
@@ -3263,6 +3302,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     qpp_desc *dd = (qpp_desc *)s->d_misc;
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
+    const double t_start = trace_now();
     const bool in_direct = in == s->h_in || host_registered(in, in_len);
     const bool out_direct = out == s->h_out || host_registered(out, out_len);
     const bool res_direct = host_registered(res, (size_t)n * sizeof(qpp_result));
@@ -3337,11 +3377,18 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         }
     }
     if (rc != QPP_OK) return rc;
+    const double t_sub = trace_now();
     for (int c = next_out; c < chunks; ++c) {
         HIPCHK(hipEventSynchronize(s->ev_out[c]));
         hand_back(c);
     }
     HIPCHK(hipStreamSynchronize(s->s_out));
+    if (trace_on()) {
+        outg.wait();
+        fprintf(stderr, "qpp session: %s %u packets %d chunks in %d out %d res %d: submit %.2f ms, wait %.2f ms (%d handed back early)\n",
+                enc ? "protect" : "unprotect", n, chunks, (int)in_direct, (int)out_direct, (int)res_direct,
+                t_sub - t_start, trace_now() - t_sub, next_out);
+    }
     return QPP_OK;
 }
 
@@ -3595,6 +3642,17 @@ static int multi_run(bool enc, qpp_multi *m, const qpp_desc *desc, uint32_t n, c
     if (n == 0) {
         if (out_len) memset(out, 0, out_len);
         return QPP_OK;
+    }
+    if (m->n == 1) {
+        // one device: the session itself (its bounds checks and staging),
+        // without the range split's copy and passes over the descriptors
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(m->device[0]);
+        const int rc = enc ? qpp_session_protect(m->s[0], m->kt[0], desc, n, in, in_len, out, out_len, res)
+                           : qpp_session_unprotect(m->s[0], m->kt[0], desc, n, in, in_len, out, out_len, res);
+        (void)hipSetDevice(prev);
+        return rc;
     }
     int parts = m->n < (int)n ? m->n : (int)n;
     // bounds first (as a session does), so that extents use only packets

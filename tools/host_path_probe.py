@@ -15,7 +15,7 @@ from aioquic_amd.batch import MultiDeviceEngine, register_host  # noqa: E402
 from aioquic_amd.bench_data import make_workload  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
-modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["staged", "registered"]
+modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["staged", "registered"]  # run in this order
 w = make_workload(n, suite=0, n_keys=1, seed=0x9001, version=1)
 eng = MultiDeviceEngine(w.n_keys, devices=[0])
 eng.set_key_records(w.keys)
