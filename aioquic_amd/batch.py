@@ -145,47 +145,6 @@ class PacketEngine:
            out.ctypes.data, out.nbytes, results.ctypes.data)
 
 
-class HostRegistration:
-    """A host array page-locked for the host-buffer calls (qpp_host_register):
-    protect_into / unprotect_into of a PacketEngine or MultiDeviceEngine whose
-    input, output or result array lies inside a registered one move it by DMA
-    straight from / to the array instead of through pinned staging.  For the
-    long-lived buffers of a server (its socket ring, asyncio/protocol.py:
-    121-122,154-158).  Keeps the array alive until close(); use as a context
-    manager or call close() before the array goes away."""
-
-    def __init__(self, arr: np.ndarray):
-        if not arr.flags.c_contiguous:
-            raise ValueError("a registered array must be contiguous")
-        self.array = arr
-        self._ptr = int(arr.ctypes.data)
-        _crypto.host_register(self._ptr, int(arr.nbytes))
-
-    def close(self) -> None:
-        if self.array is not None:
-            _crypto.host_unregister(self._ptr)
-            self.array = None
-
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *exc) -> None:
-        self.close()
-
-
-def register_host(*arrays: np.ndarray) -> list:
-    """HostRegistration of each array (close them when done)."""
-    regs = []
-    try:
-        for a in arrays:
-            regs.append(HostRegistration(a))
-    except Exception:
-        for r in regs:
-            r.close()
-        raise
-    return regs
-
-
 class MultiDeviceEngine:
     """Host-buffer batches split over several GPUs of the node (qpp_multi):
     the batch's descriptors are cut into contiguous ranges, one per device,

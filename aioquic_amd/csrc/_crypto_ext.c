@@ -1793,31 +1793,6 @@ static PyObject *py_watchdog(PyObject *m, PyObject *unused)
     return PyLong_FromUnsignedLong(v);
 }
 
-/* host_register(ptr, len) / host_unregister(ptr): qpp_host_register */
-static PyObject *py_host_register(PyObject *m, PyObject *args)
-{
-    unsigned long long ptr, len;
-    int rc;
-    if (!PyArg_ParseTuple(args, "KK", &ptr, &len)) return NULL;
-    Py_BEGIN_ALLOW_THREADS
-    rc = qpp_host_register((void *)(uintptr_t)ptr, (size_t)len);
-    Py_END_ALLOW_THREADS
-    if (check_rc(rc) < 0) return NULL;
-    Py_RETURN_NONE;
-}
-
-static PyObject *py_host_unregister(PyObject *m, PyObject *args)
-{
-    unsigned long long ptr;
-    int rc;
-    if (!PyArg_ParseTuple(args, "K", &ptr)) return NULL;
-    Py_BEGIN_ALLOW_THREADS
-    rc = qpp_host_unregister((void *)(uintptr_t)ptr);
-    Py_END_ALLOW_THREADS
-    if (check_rc(rc) < 0) return NULL;
-    Py_RETURN_NONE;
-}
-
 #ifndef QPP_SOURCE_HASH
 #error "build with -DQPP_SOURCE_HASH (aioquic_amd/build.py)"
 #endif
@@ -1851,9 +1826,6 @@ static PyMethodDef module_methods[] = {
      "receive_short(table, items, conns, conn_cid_u32, conn_pair_u32, conn_space_u32, pair_slot_u32, space_exp_u64, "
      "rec_type, packet_type, epoch) -> None | (records, deferred, space_exp)"},
     {"hp_mask_host", py_hp_mask_host, METH_VARARGS, "hp_mask_host(table, slots_u32, samples) -> masks"},
-    {"host_register", py_host_register, METH_VARARGS,
-     "host_register(ptr, len): page-lock caller memory for direct DMA by the host-buffer calls"},
-    {"host_unregister", py_host_unregister, METH_VARARGS, "host_unregister(ptr)"},
     {"device_ok", py_device_ok, METH_NOARGS, "True when a gfx950 device is usable"},
     {"abi_version", py_abi, METH_NOARGS, "C ABI version of libquicpp"},
     {"watchdog_count", py_watchdog, METH_NOARGS, "GCM table-entry watchdog events on the current device (0 expected)"},

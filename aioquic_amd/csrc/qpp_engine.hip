@@ -3048,8 +3048,8 @@ class CopyPool {
     };
     CopyPool()
     {
-        const char *v = getenv("QPP_COPY_THREADS");  // A/B switch, default 8
-        const int t = v ? atoi(v) : 8;
+        const char *v = getenv("QPP_COPY_THREADS");  // A/B switch, default 6
+        const int t = v ? atoi(v) : 6;
         n_ = t < 1 ? 1 : t > 32 ? 32 : t;
         for (int i = 0; i < n_; ++i) std::thread([this] { run(); }).detach();
     }
@@ -3137,140 +3137,6 @@ static int session_launch(bool enc, qpp_session *s, const qpp_keytab *kt, const 
     return rc;
 }
 
-// Registered host buffers (qpp_host_register): page-locked caller memory
-// that the pipelined session path moves by DMA directly.  Pinning works on
-// whole pages, and two small arrays may share a page, so a request is pinned
-// as up to three pieces -- its first page, its interior, its last page --
-// each a hipHostRegister of its own: only a boundary page can be shared with
-// another live array, and it is then one piece held by both (reference
-// count), while the interior belongs to the request alone and is unpinned
-// with it (so no pin outlives the memory it was taken on).  A transfer goes
-// direct when pieces cover it, cut at piece boundaries (one runtime
-// registration per copy).
-struct HostPiece {
-    uintptr_t lo, hi;
-    int refs;
-};
-struct HostReq {
-    uintptr_t key, lo, hi;
-};
-constexpr uintptr_t kPage = 4096;
-static std::mutex g_host_mu;
-static std::vector<HostPiece> g_pieces;  // disjoint, sorted by lo
-static std::vector<HostReq> g_reqs;
-
-// The pieces covering [a, b) in order, or empty when some byte is not pinned.
-static std::vector<std::pair<uintptr_t, uintptr_t>> host_cover(const void *p, size_t len)
-{
-    std::vector<std::pair<uintptr_t, uintptr_t>> out;
-    uintptr_t a = (uintptr_t)p;
-    const uintptr_t b = a + len;
-    std::lock_guard<std::mutex> g(g_host_mu);
-    for (const HostPiece &r : g_pieces) {
-        if (a >= b) break;
-        if (r.hi <= a) continue;
-        if (r.lo > a) return {};
-        const uintptr_t e = r.hi < b ? r.hi : b;
-        out.emplace_back(a, e);
-        a = e;
-    }
-    if (a < b) return {};
-    return out;
-}
-
-static bool host_registered(const void *p, size_t len) { return len == 0 || !host_cover(p, len).empty(); }
-
-// hipMemcpyAsync with the host side cut at piece boundaries (registered
-// caller memory).  D2H is left to the runtime, which moves it by a blit
-// kernel beside the copy engines' H2D (forcing the copy engines with
-// DeviceToDeviceNoCU measured slower on the pipeline: both directions then
-// share them, profiles/r5g_d2h_engines.txt).
-static hipError_t copy_pinned(void *dst, const void *src, size_t n, hipMemcpyKind kind, hipStream_t st)
-{
-    const bool h2d = kind == hipMemcpyHostToDevice;
-    const uint8_t *host = (const uint8_t *)(h2d ? src : dst);
-    const auto parts = host_cover(host, n);
-    if (parts.empty()) return hipMemcpyAsync(dst, src, n, kind, st);
-    for (const auto &pc : parts) {
-        const size_t off = pc.first - (uintptr_t)host, len = pc.second - pc.first;
-        const hipError_t e = hipMemcpyAsync((uint8_t *)dst + off, (const uint8_t *)src + off, len, kind, st);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
-int qpp_host_register(void *ptr, size_t len)
-{
-    if (!ptr || !len) return QPP_E_ARG;
-    const uintptr_t lo = (uintptr_t)ptr & ~(kPage - 1), hi = ((uintptr_t)ptr + len + kPage - 1) & ~(kPage - 1);
-    // the pieces this request needs: first page, interior, last page
-    std::vector<HostPiece> want;
-    want.push_back(HostPiece{lo, lo + kPage, 0});
-    if (hi - lo > 2 * kPage) want.push_back(HostPiece{lo + kPage, hi - kPage, 0});
-    if (hi - lo > kPage) want.push_back(HostPiece{hi - kPage, hi, 0});
-    std::lock_guard<std::mutex> g(g_host_mu);
-    for (const HostReq &q : g_reqs)
-        if (q.key == (uintptr_t)ptr) return QPP_E_ARG;  // registered already
-    // each wanted piece exists as it is (a shared boundary page) or meets
-    // no piece at all; anything else overlaps another registered range
-    std::vector<bool> have(want.size(), false);
-    for (size_t i = 0; i < want.size(); ++i)
-        for (const HostPiece &r : g_pieces) {
-            if (r.hi <= want[i].lo || r.lo >= want[i].hi) continue;
-            if (r.lo == want[i].lo && r.hi == want[i].hi && want[i].hi - want[i].lo == kPage) {
-                have[i] = true;
-                continue;
-            }
-            return QPP_E_ARG;
-        }
-    for (size_t i = 0; i < want.size(); ++i) {
-        if (have[i]) continue;
-        static const unsigned reg_flags = [] {
-            const char *v = getenv("QPP_REG_FLAGS");  // study switch (round 5)
-            return v ? (unsigned)strtoul(v, nullptr, 0) : (unsigned)hipHostRegisterPortable;
-        }();
-        if (hipHostRegister((void *)want[i].lo, want[i].hi - want[i].lo, reg_flags) != hipSuccess) {
-            (void)hipGetLastError();
-            for (size_t j = 0; j < i; ++j)
-                if (!have[j]) (void)hipHostUnregister((void *)want[j].lo);
-            (void)hipGetLastError();
-            return QPP_E_HIP;
-        }
-    }
-    for (size_t i = 0; i < want.size(); ++i)
-        if (!have[i]) g_pieces.push_back(want[i]);
-    std::sort(g_pieces.begin(), g_pieces.end(), [](const HostPiece &x, const HostPiece &y) { return x.lo < y.lo; });
-    for (HostPiece &r : g_pieces)
-        if (r.lo < hi && r.hi > lo) ++r.refs;
-    g_reqs.push_back(HostReq{(uintptr_t)ptr, lo, hi});
-    return QPP_OK;
-}
-
-int qpp_host_unregister(void *ptr)
-{
-    std::lock_guard<std::mutex> g(g_host_mu);
-    for (size_t i = 0; i < g_reqs.size(); ++i) {
-        if (g_reqs[i].key != (uintptr_t)ptr) continue;
-        const uintptr_t lo = g_reqs[i].lo, hi = g_reqs[i].hi;
-        g_reqs.erase(g_reqs.begin() + (ptrdiff_t)i);
-        int rc = QPP_OK;
-        for (size_t k = 0; k < g_pieces.size();) {
-            HostPiece &r = g_pieces[k];
-            if (r.lo < hi && r.hi > lo && --r.refs == 0) {
-                if (hipHostUnregister((void *)r.lo) != hipSuccess) {
-                    (void)hipGetLastError();
-                    rc = QPP_E_HIP;
-                }
-                g_pieces.erase(g_pieces.begin() + (ptrdiff_t)k);
-                continue;
-            }
-            ++k;
-        }
-        return rc;
-    }
-    return QPP_E_ARG;
-}
-
 // QPP_SESSION_TRACE=1: one stderr line per pipelined call with its host
 // phases (a study switch, read once per process)
 static bool trace_on()
@@ -3285,14 +3151,18 @@ static double trace_now()
 }
 
 // Chunk c of the batch: its descriptors are copied into pinned staging and
-// bounds-checked by the host, and they and the chunk's input extent go H2D on
-// s_in (from the caller's memory when it is registered, else after a host
-// copy into pinned staging); the chunk's kernels run on the kernel stream
-// once that lands; its output tile and results go D2H on s_out (into the
-// caller's memory when registered), and are copied out by the host while
-// later chunks are in flight.  So host copies, both PCIe directions and the
-// kernels of different chunks overlap, and no work on the whole batch
-// precedes the first chunk's copies.
+// bounds-checked by the host, its input extent is copied into pinned staging
+// by the copy pool, and both go H2D on s_in (the copy engines); the chunk's
+// kernels run on the kernel stream once that lands; its output tile and
+// results go D2H on s_out (a blit kernel, the runtime's choice, which runs
+// beside the packet kernels: profiles/r5g_d2h_engines.txt), and the pool
+// copies them out while later chunks are in flight.  So host copies, both
+// PCIe directions and the kernels of different chunks overlap, and no work
+// on the whole batch precedes the first chunk's copies.  (Round 5 also built
+// DMA straight from / to caller memory pinned by hipHostRegister: correct,
+// but 9.6-10.7 GiB/s against 17-19 GiB/s for this staged pipeline on the
+// same boxes whatever the flags and D2H form, so it was removed;
+// profiles/r5e_host_path/.)
 static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
                                  const qpp_desc *desc, uint32_t n, const uint8_t *in,
                                  size_t in_len, uint8_t *out, size_t out_len, qpp_result *res,
@@ -3303,12 +3173,9 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     qpp_desc *dd = (qpp_desc *)s->d_misc;
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     const double t_start = trace_now();
-    const bool in_direct = in == s->h_in || host_registered(in, in_len);
-    const bool out_direct = out == s->h_out || host_registered(out, out_len);
-    const bool res_direct = host_registered(res, (size_t)n * sizeof(qpp_result));
-    const uint8_t *h_src = in_direct ? in : s->h_in;
-    uint8_t *h_dst = out_direct ? out : s->h_out;
-    qpp_result *h_res = res_direct ? res : hr;
+    // the caller may have assembled its input / wants its output in the
+    // session's own staging (qpp_session_stage): no host copy then
+    const bool in_direct = in == s->h_in, out_direct = out == s->h_out;
     HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     size_t olo[kPipeMaxChunks + 1];
     uint32_t first[kPipeMaxChunks + 1];
@@ -3327,8 +3194,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     auto hand_back = [&](int d) {
         if (olo[d + 1] > olo[d] && !out_direct)
             par_memcpy(out + olo[d], s->h_out + olo[d], olo[d + 1] - olo[d], &outg);
-        if (!res_direct)
-            memcpy(res + first[d], hr + first[d], (size_t)(first[d + 1] - first[d]) * sizeof(qpp_result));
+        memcpy(res + first[d], hr + first[d], (size_t)(first[d + 1] - first[d]) * sizeof(qpp_result));
     };
     int rc = QPP_OK;
     int next_out = 0;
@@ -3350,7 +3216,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         if (hi > in_len) hi = in_len;
         if (lo < hi) {
             if (!in_direct) par_memcpy(s->h_in + lo, in + lo, hi - lo);
-            HIPCHK(copy_pinned(s->d_in + lo, h_src + lo, hi - lo, hipMemcpyHostToDevice, s->s_in));
+            HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice, s->s_in));
         }
         HIPCHK(hipEventRecord(s->ev_in[c], s->s_in));
         HIPCHK(hipStreamWaitEvent(s->stream, s->ev_in[c], 0));
@@ -3361,10 +3227,10 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         HIPCHK(hipEventRecord(s->ev_k[c], s->stream));
         HIPCHK(hipStreamWaitEvent(s->s_out, s->ev_k[c], 0));
         if (olo[c + 1] > olo[c])
-            HIPCHK(copy_pinned(h_dst + olo[c], s->d_out + olo[c], olo[c + 1] - olo[c], hipMemcpyDeviceToHost,
+            HIPCHK(hipMemcpyAsync(s->h_out + olo[c], s->d_out + olo[c], olo[c + 1] - olo[c], hipMemcpyDeviceToHost,
                                s->s_out));
         if (b > a)
-            HIPCHK(copy_pinned(h_res + a, dr + a, (size_t)(b - a) * sizeof(qpp_result), hipMemcpyDeviceToHost,
+            HIPCHK(hipMemcpyAsync(hr + a, dr + a, (size_t)(b - a) * sizeof(qpp_result), hipMemcpyDeviceToHost,
                                s->s_out));
         HIPCHK(hipEventRecord(s->ev_out[c], s->s_out));
         // hand back chunks whose D2H has already landed while later ones fly
@@ -3385,8 +3251,8 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     HIPCHK(hipStreamSynchronize(s->s_out));
     if (trace_on()) {
         outg.wait();
-        fprintf(stderr, "qpp session: %s %u packets %d chunks in %d out %d res %d: submit %.2f ms, wait %.2f ms (%d handed back early)\n",
-                enc ? "protect" : "unprotect", n, chunks, (int)in_direct, (int)out_direct, (int)res_direct,
+        fprintf(stderr, "qpp session: %s %u packets %d chunks in %d out %d: submit %.2f ms, wait %.2f ms (%d handed back early)\n",
+                enc ? "protect" : "unprotect", n, chunks, (int)in_direct, (int)out_direct,
                 t_sub - t_start, trace_now() - t_sub, next_out);
     }
     return QPP_OK;

@@ -677,11 +677,17 @@ def main():
         if w.n_keys >= 64:
             out["key_schedule"] = key_schedule(PacketEngine, w.n_keys, cfg["suite"], cfg["version"])
         if args.e2e:
+            # the PCIe legs start from a clean host and device: the timed
+            # region's buffers go first (host and device memory they held
+            # otherwise sits beside the legs' own multi-GiB buffers)
+            del d_plain, d_desc, d_udesc, d_wire, d_back, d_r1, d_r2, w
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+            if world == 1:
+                out["e2e_host_devices"] = e2e_host_devices(cfg, seed, args.e2e_packets)
             out["e2e"] = e2e(PacketEngine, cfg, seed, dev, args.e2e_packets,
                              chunks=args.e2e_chunks, n_streams=args.e2e_streams,
                              mode=args.e2e_mode)
-            if world == 1:
-                out["e2e_host_devices"] = e2e_host_devices(cfg, seed, args.e2e_packets)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -708,12 +714,10 @@ def e2e_host_devices(cfg, seed, n, reps=3):
     (MultiDeviceEngine / qpp_multi: one host batch cut into contiguous ranges,
     one session and key-table replica per device, host threads in parallel):
     host memory -> protect -> host, then host -> unprotect -> host, per device
-    count 1..D, with plain pageable arrays (copied through the session's
-    pinned staging, `gib_s`) and with the arrays registered
-    (qpp_host_register: DMA straight from / to them, `registered_gib_s`).
-    PCIe-inclusive; never the bench value."""
+    count 1..D, from and into caller-owned pageable arrays.  PCIe-inclusive;
+    never the bench value."""
     import torch
-    from aioquic_amd.batch import MultiDeviceEngine, register_host
+    from aioquic_amd.batch import MultiDeviceEngine
     from aioquic_amd.bench_data import make_workload
 
     w = make_workload(n, suite=cfg["suite"], n_keys=cfg["n_keys"], seed=seed, version=cfg["version"],
@@ -724,8 +728,9 @@ def e2e_host_devices(cfg, seed, n, reps=3):
     back = np.empty(w.plain_size, np.uint8)
     r1 = np.empty(n, L_RESULT())
     r2 = np.empty(n, L_RESULT())
-
-    def run(eng):
+    for d in range(1, torch.cuda.device_count() + 1):
+        eng = MultiDeviceEngine(w.n_keys, devices=list(range(d)))
+        eng.set_key_records(w.keys)
         eng.protect_into(w.desc, plain, wire, r1)  # warm-up (staging allocation, first touch)
         eng.unprotect_into(w.udesc, wire, back, r2)
         times = []
@@ -736,29 +741,12 @@ def e2e_host_devices(cfg, seed, n, reps=3):
             eng.unprotect_into(w.udesc, wire, back, r2)
             times.append(time.perf_counter() - t0)
         ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all() and np.array_equal(back, plain))
-        return round(n * 1200 / float(np.median(times)) / GIB, 3), ok
-
-    for d in range(1, torch.cuda.device_count() + 1):
-        eng = MultiDeviceEngine(w.n_keys, devices=list(range(d)))
-        eng.set_key_records(w.keys)
-        staged, ok_s = run(eng)
-        t0 = time.perf_counter()
-        regs = register_host(plain, wire, back, r1, r2)
-        reg_ms = (time.perf_counter() - t0) * 1e3
-        try:
-            direct, ok_d = run(eng)
-        finally:
-            for r in regs:
-                r.close()
-        out[str(d)] = {"gib_s": staged, "round_trip_ok": ok_s and ok_d, "registered_gib_s": direct,
-                       "register_ms": round(reg_ms, 1)}
+        out[str(d)] = {"gib_s": round(n * 1200 / float(np.median(times)) / GIB, 3), "round_trip_ok": ok}
         del eng
     return {"per_device_count": out, "packets": n,
-            "note": "caller-owned host arrays: qpp_multi protect_into, then unprotect_into (two synchronous "
-                    "calls; each a chunked H2D / kernel / D2H pipeline). gib_s: pageable arrays copied through "
-                    "the library's pinned staging by its copy threads; registered_gib_s: the same arrays "
-                    "registered (qpp_host_register, register_ms) and moved by DMA straight from / to them, "
-                    "measured after the staged run"}
+            "note": "caller-owned pageable host arrays: qpp_multi protect_into, then unprotect_into (two "
+                    "synchronous calls; each a chunked pipeline: host copy into pinned staging by the library's "
+                    "copy threads, H2D, kernels, D2H, copy out)"}
 
 
 def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5, mode="staged"):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define QPP_ABI_VERSION 4
+#define QPP_ABI_VERSION 3
 
 /* cipher suites (quic/crypto.py:12-16 CIPHER_SUITES) */
 #define QPP_AES_128_GCM 0        /* aes-128-gcm + aes-128-ecb header protection */
@@ -232,20 +232,6 @@ int qpp_session_stage(qpp_session *s, size_t bytes, uint32_t n, uint8_t **h_in, 
 int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material *km,
                          uint32_t n);
 
-/* Registered host buffers (ABI 4).  A server's socket buffers are long-lived
- * (the datagrams of src/aioquic/asyncio/protocol.py:121-122,154-158 arrive in
- * and leave from them), so a caller may pin them once: qpp_host_register
- * page-locks [ptr, ptr + len) for every device (hipHostRegister, portable).
- * A session call whose input, output or result array lies inside a registered
- * range moves it by DMA straight from / to the caller's memory instead of
- * copying it through the session's pinned staging (the bytes written are the
- * same).  Two ranges may share a boundary page (pinned once, reference-
- * counted); a range that overlaps a registered one otherwise, or the same ptr
- * twice, is refused (QPP_E_ARG) -- a sub-range of a registered array needs
- * no registration of its own.  The range must stay allocated until
- * qpp_host_unregister(ptr) with the same ptr.  Thread-safe. */
-int qpp_host_register(void *ptr, size_t len);
-int qpp_host_unregister(void *ptr);
 
 /* One host batch over several GPUs of the node (the
  * server socket of src/aioquic/asyncio/server.py:60-152 feeds all

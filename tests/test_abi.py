@@ -46,7 +46,7 @@ def test_library_loads_and_reports_abi():
     for n in declared_functions():
         getattr(lib, n)
     lib.qpp_abi_version.restype = ctypes.c_int
-    assert lib.qpp_abi_version() == 4
+    assert lib.qpp_abi_version() == 3
     lib.qpp_strerror.restype = ctypes.c_char_p
     lib.qpp_strerror.argtypes = [ctypes.c_int]
     assert lib.qpp_strerror(0)

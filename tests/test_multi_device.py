@@ -104,66 +104,3 @@ def test_multi_empty_middle_range_out_of_order():
     b = multi.protect_host(d, w.plain, w.wire_size)
     assert (a[1]["status"][300:600] == L.S_LENGTH).all() and (a[1]["status"][:300] == L.S_OK).all()
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
-
-
-@pytest.mark.parametrize("devices", [[0], [0, 0]], ids=["1-session", "2-sessions"])
-def test_registered_host_buffers(devices):
-    """Registered caller arrays (qpp_host_register, ABI 4): a pipelined batch
-    (>= 64 MiB of output) moves its input, output and results by DMA straight
-    from / to the caller's arrays; the bytes and results equal the staged
-    path's, with a rejected descriptor and a failed tag inside, and
-    unregistering restores the staged path."""
-    from aioquic_amd import layout as L
-    from aioquic_amd.batch import MultiDeviceEngine, register_host
-
-    n = 65536 + 77  # 78 MB of 1200-byte packets: the session's pipelined path
-    w = _workload(n, 0x53)
-    eng = MultiDeviceEngine(w.n_keys, devices=devices)
-    eng.set_key_records(w.keys)
-    d = w.desc.copy()
-    d[1234]["in_off"] = w.plain_size + 1  # rejected: QPP_S_LENGTH, nothing touched
-    plain = w.plain.copy()
-    outs = {}
-    for mode in ("staged", "registered"):
-        wire = np.full(w.wire_size, 0xA5, np.uint8)
-        back = np.full(w.plain_size, 0x5A, np.uint8)
-        r1 = np.zeros(n, L.RESULT)
-        r2 = np.zeros(n, L.RESULT)
-        regs = register_host(plain, wire, back, r1, r2) if mode == "registered" else []
-        try:
-            eng.protect_into(d, plain, wire, r1)
-            bad = wire.copy()
-            bad[int(w.udesc[4321]["in_off"]) + 100] ^= 0x10  # a failed tag
-            if regs:
-                regs.append(register_host(bad)[0])
-            eng.unprotect_into(w.udesc, bad, back, r2)
-        finally:
-            for r in regs:
-                r.close()
-        assert r1[1234]["status"] == L.S_LENGTH
-        assert (np.delete(r1["status"], 1234) == L.S_OK).all()
-        assert r2[4321]["status"] == L.S_DECRYPT
-        outs[mode] = (wire, back, r1, r2)
-    a, b = outs["staged"], outs["registered"]
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
-    # registration rules: the same array twice, or a large view overlapping a
-    # registered array's interior, is refused; small arrays sharing a page
-    # are pinned once and released by reference count
-    big = np.zeros(1 << 20, np.uint8)
-    smalls = [np.zeros(100 + i, np.uint8) for i in range(8)]
-    with register_host(big)[0]:
-        with pytest.raises(RuntimeError):
-            register_host(big)
-        with pytest.raises(RuntimeError):
-            register_host(big[5000:])
-        regs = register_host(*smalls)
-        for r in regs[::2]:
-            r.close()
-        for r in regs[1::2]:
-            r.close()
-    # every packet except the rejected one and the forged one came back
-    ok = np.ones(n, bool)
-    ok[[1234, 4321]] = False
-    rows = a[1].reshape(n, 1200)[ok]
-    assert np.array_equal(rows, w.plain.reshape(n, 1200)[ok])

@@ -1,5 +1,6 @@
 """The library's host-buffer path (MultiDeviceEngine on one device) with the
-caller's arrays staged (pageable) or registered (qpp_host_register): 1 Mi
+caller's arrays staged (pageable) or registered (the round-5 qpp_host_register
+study, since removed: mode "registered" needs that build): 1 Mi
 north-star packets, protect_into + unprotect_into, a few reps each, timed per
 call.  For rocprofv3 runs (which copy engine / blit kernel moves the bytes)."""
 import json
@@ -11,7 +12,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from aioquic_amd import layout as L  # noqa: E402
-from aioquic_amd.batch import MultiDeviceEngine, register_host  # noqa: E402
+from aioquic_amd.batch import MultiDeviceEngine  # noqa: E402
 from aioquic_amd.bench_data import make_workload  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
@@ -26,7 +27,11 @@ r1 = np.empty(n, L.RESULT)
 r2 = np.empty(n, L.RESULT)
 out = {}
 for mode in modes:
-    regs = register_host(plain, wire, back, r1, r2) if mode == "registered" else []
+    if mode == "registered":
+        from aioquic_amd.batch import register_host  # the removed study API
+        regs = register_host(plain, wire, back, r1, r2)
+    else:
+        regs = []
     ts = []
     for rep in range(4):
         t0 = time.perf_counter()
