@@ -2371,6 +2371,11 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 #include <string.h>
 
 #include <algorithm>
+#include <ctype.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
+
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -2412,9 +2417,12 @@ static uint32_t keytab_suite_mask(const qpp_keytab *kt)
 
 // Host batches of at least 2 x kPipeChunkBytes of output go through the
 // session as a three-stage pipeline of up to kPipeMaxChunks chunks (see
-// session_run_pipelined).
+// session_run_pipelined): up to kPipeRegular chunks of about equal size, the
+// first and last of them cut into quarter, quarter and half (kPipeTaper) so
+// the pipeline fills and drains on small pieces.
 constexpr size_t kPipeChunkBytes = (size_t)32 << 20;
-constexpr int kPipeMaxChunks = 32;
+constexpr int kPipeRegular = 32, kPipeTaper = 2;
+constexpr int kPipeMaxChunks = kPipeRegular + 2 * kPipeTaper;
 constexpr int kMultiMaxDevices = 16;  // qpp_multi: devices per host-batch engine
 
 struct qpp_session {
@@ -3022,7 +3030,19 @@ class CopyPool {
   public:
     static CopyPool &get()
     {
-        static CopyPool *p = new CopyPool();  // never destroyed: no join at exit
+        // never destroyed (no join at exit); a forked child, which inherits
+        // the pointer but not the threads, starts a pool of its own
+        static std::once_flag once;
+        std::call_once(once, [] { pthread_atfork(nullptr, nullptr, [] { g_pool.store(nullptr); }); });
+        CopyPool *p = g_pool.load();
+        if (!p) {
+            std::lock_guard<std::mutex> l(g_pool_mu);
+            p = g_pool.load();
+            if (!p) {
+                p = new CopyPool();
+                g_pool.store(p);
+            }
+        }
         return *p;
     }
     int threads() const { return n_; }
@@ -3051,7 +3071,56 @@ class CopyPool {
         const char *v = getenv("QPP_COPY_THREADS");  // A/B switch, default 6
         const int t = v ? atoi(v) : 6;
         n_ = t < 1 ? 1 : t > 32 ? 32 : t;
-        for (int i = 0; i < n_; ++i) std::thread([this] { run(); }).detach();
+        // the threads run on the CPUs of the current device's NUMA node,
+        // where its pinned staging sits (a two-socket host otherwise moves
+        // the copies across sockets); QPP_COPY_NUMA=0 leaves them anywhere
+        const char *nv = getenv("QPP_COPY_NUMA");
+        cpu_set_t set;
+        const bool pin = !(nv && nv[0] == '0') && device_node_cpus(&set);
+        for (int i = 0; i < n_; ++i) {
+            std::thread th([this] { run(); });
+            if (pin) (void)pthread_setaffinity_np(th.native_handle(), sizeof set, &set);
+            th.detach();
+        }
+    }
+    // the CPUs of the current device's NUMA node (sysfs), within this
+    // process's affinity; false when unknown
+    static bool device_node_cpus(cpu_set_t *set)
+    {
+        int dev = 0;
+        char bus[64] = {0};
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        for (char *c = bus; *c; ++c) *c = (char)tolower(*c);
+        char path[160];
+        snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+        FILE *f = fopen(path, "r");
+        if (!f) return false;
+        int node = -1;
+        if (fscanf(f, "%d", &node) != 1) node = -1;
+        fclose(f);
+        if (node < 0) return false;
+        snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+        f = fopen(path, "r");
+        if (!f) return false;
+        cpu_set_t own;
+        if (sched_getaffinity(0, sizeof own, &own) != 0) CPU_ZERO(&own);
+        CPU_ZERO(set);
+        int a, b, n = 0;
+        while (fscanf(f, "%d", &a) == 1) {
+            b = a;
+            if (fscanf(f, "-%d", &b) != 1) b = a;
+            for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+                if (CPU_ISSET(c, &own)) {
+                    CPU_SET(c, set);
+                    ++n;
+                }
+            if (fgetc(f) != ',') break;
+        }
+        fclose(f);
+        return n > 0;
     }
     void run()
     {
@@ -3076,7 +3145,11 @@ class CopyPool {
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<Task> q_;
+    static std::atomic<CopyPool *> g_pool;
+    static std::mutex g_pool_mu;
 };
+std::atomic<CopyPool *> CopyPool::g_pool{nullptr};
+std::mutex CopyPool::g_pool_mu;
 
 // dst <- src over the pool's threads in parts of >= 4 MiB; with g, return at
 // once (g->wait() before the bytes are used), else when the copy is done.
@@ -3179,8 +3252,22 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     size_t olo[kPipeMaxChunks + 1];
     uint32_t first[kPipeMaxChunks + 1];
+    // chunk weights in quarters of a regular chunk: 1, 1, 2 at the start and
+    // 2, 1, 1 at the end when there are enough regular chunks to taper
+    const int regular = chunks;
+    const bool taper = regular >= 8;
+    if (taper) chunks = regular + 2 * kPipeTaper;
+    auto weight = [&](int c) -> uint64_t {
+        if (!taper) return 4;
+        if (c < 3) return c < 2 ? 1 : 2;
+        if (c >= chunks - 3) return c >= chunks - 2 ? 1 : 2;
+        return 4;
+    };
+    const uint64_t wsum = 4ull * (uint64_t)regular;
+    uint64_t wacc = 0;
     for (int c = 0; c <= chunks; ++c) {
-        first[c] = (uint32_t)((uint64_t)n * c / chunks);
+        first[c] = (uint32_t)((uint64_t)n * wacc / wsum);
+        if (c < chunks) wacc += weight(c);
         olo[c] = c == 0 ? 0 : c == chunks ? out_len : (size_t)desc[first[c]].out_off;
         if (olo[c] > out_len) olo[c] = out_len;
     }
@@ -3285,7 +3372,7 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
     int rc = session_reserve(s, need, n);
     if (rc != QPP_OK) return rc;
     size_t want = out_len / kPipeChunkBytes;
-    int chunks = want > (size_t)kPipeMaxChunks ? kPipeMaxChunks : (int)want;
+    int chunks = want > (size_t)kPipeRegular ? kPipeRegular : (int)want;
     if (chunks > (int)n) chunks = (int)n;
     const char *serial = getenv("QPP_SESSION_SERIAL");  // A/B switch: "1" = serial path
     if (chunks >= 2 && !(serial && serial[0] == '1')) {

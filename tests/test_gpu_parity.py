@@ -512,10 +512,13 @@ def test_fused_protect_length_boundary(oracle, L, engine_cls):
         hp.apply(b"\x40" + bytes(10), bytes(1490))
 
 
-@pytest.mark.parametrize("mixed", [False, True])
-def test_session_pipelined_host_batch(L, engine_cls, mixed):
+@pytest.mark.parametrize("mixed,n", [(False, 98304), (True, 98304), (False, 262144)],
+                         ids=["3-chunks", "3-chunks-mixed", "tapered-13-chunks"])
+def test_session_pipelined_host_batch(L, engine_cls, mixed, n):
     """Host-buffer batches of >= 64 MiB go through the session's three-stage
-    pipeline (chunked H2D / kernels / D2H, qpp_engine.hip session_run_pipelined).
+    pipeline (chunked H2D / kernels / D2H, qpp_engine.hip session_run_pipelined;
+    from 8 regular chunks on, the first and last are cut into quarter /
+    quarter / half pieces: 262144 packets, 315 MB, run as 13 chunks).
     Its output and results must equal the serial session path
     (QPP_SESSION_SERIAL=1) and the device-resident path byte for byte; a
     tampered packet in a late chunk reports its status in place; a
@@ -524,7 +527,6 @@ def test_session_pipelined_host_batch(L, engine_cls, mixed):
 
     from aioquic_amd import bench_data
 
-    n = 98304  # 118 MB of wire: 3 pipeline chunks
     kw = dict(mixed=[0, 2]) if mixed else {}
     w = bench_data.make_workload(n, suite=0, n_keys=7, seed=0x51 + int(mixed), **kw)
     eng = engine_cls(w.n_keys)
