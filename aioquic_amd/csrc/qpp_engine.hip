@@ -2371,10 +2371,7 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 #include <string.h>
 
 #include <algorithm>
-#include <ctype.h>
 #include <pthread.h>
-#include <sched.h>
-#include <stdio.h>
 
 #include <atomic>
 #include <chrono>
@@ -3071,56 +3068,11 @@ class CopyPool {
         const char *v = getenv("QPP_COPY_THREADS");  // A/B switch, default 6
         const int t = v ? atoi(v) : 6;
         n_ = t < 1 ? 1 : t > 32 ? 32 : t;
-        // the threads run on the CPUs of the current device's NUMA node,
-        // where its pinned staging sits (a two-socket host otherwise moves
-        // the copies across sockets); QPP_COPY_NUMA=0 leaves them anywhere
-        const char *nv = getenv("QPP_COPY_NUMA");
-        cpu_set_t set;
-        const bool pin = !(nv && nv[0] == '0') && device_node_cpus(&set);
-        for (int i = 0; i < n_; ++i) {
-            std::thread th([this] { run(); });
-            if (pin) (void)pthread_setaffinity_np(th.native_handle(), sizeof set, &set);
-            th.detach();
-        }
-    }
-    // the CPUs of the current device's NUMA node (sysfs), within this
-    // process's affinity; false when unknown
-    static bool device_node_cpus(cpu_set_t *set)
-    {
-        int dev = 0;
-        char bus[64] = {0};
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        for (char *c = bus; *c; ++c) *c = (char)tolower(*c);
-        char path[160];
-        snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
-        FILE *f = fopen(path, "r");
-        if (!f) return false;
-        int node = -1;
-        if (fscanf(f, "%d", &node) != 1) node = -1;
-        fclose(f);
-        if (node < 0) return false;
-        snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
-        f = fopen(path, "r");
-        if (!f) return false;
-        cpu_set_t own;
-        if (sched_getaffinity(0, sizeof own, &own) != 0) CPU_ZERO(&own);
-        CPU_ZERO(set);
-        int a, b, n = 0;
-        while (fscanf(f, "%d", &a) == 1) {
-            b = a;
-            if (fscanf(f, "-%d", &b) != 1) b = a;
-            for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
-                if (CPU_ISSET(c, &own)) {
-                    CPU_SET(c, set);
-                    ++n;
-                }
-            if (fgetc(f) != ',') break;
-        }
-        fclose(f);
-        return n > 0;
+        // (round 5 also pinned the threads to the CPUs of the device's NUMA
+        // node: 13.0-16.6 against 11.5-17.7 GiB/s unpinned on one two-socket
+        // box, interleaved -- no difference through the run-to-run spread,
+        // profiles/r5e_host_path/host_path_studies.txt; removed)
+        for (int i = 0; i < n_; ++i) std::thread([this] { run(); }).detach();
     }
     void run()
     {
