@@ -591,7 +591,9 @@ __device__ __forceinline__ void write_header_v(const Pkt &P, int sub, bool maske
 // one of the workgroup's LDS table entries; the few multiplies outside the
 // loop (associated data beyond 16 bytes by H^1, each lane's closing H^(4-j))
 // read the slot's tables in global memory.
-template <int NR, bool ENC, int BPL, int SUITE>
+// PRIO (k_gcm with 512-thread workgroups: launches of at most one item per
+// wave): the step loop sets the wave's issue priority by its progress.
+template <int NR, bool ENC, int BPL, int SUITE, bool PRIO>
 __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, const u32x4 h0,
                                             const uint32_t *rk, int sub, const GhashTabs &G,
                                             const uint8_t *te, const Bufs &B, uint32_t ioff, uint32_t ooff,
@@ -771,7 +773,23 @@ __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, con
             // the first step is peeled: it alone may carry Z and the HP sample
             one2(S, std::true_type{});
 #pragma unroll 1
-            for (int k = S - 1; k > 0; --k) one2(k, std::false_type{});
+            for (int k = S - 1; k > 0; --k) {
+                if constexpr (PRIO) {
+                    // waves further from the item's end issue first (the
+                    // sequencer arbitrates by priority, then age), so a
+                    // launch's waves progress together instead of oldest
+                    // first, and its tail of half-empty CUs shortens:
+                    // +3-5 % at 64 Ki (profiles/r5y_gcm_priority.txt; with
+                    // persistent 1024-thread workgroups, for every item or
+                    // only each share's last ones, no gain at 1 Mi)
+                    const int kr = __builtin_amdgcn_readfirstlane(k);
+                    if (kr >= 7) __builtin_amdgcn_s_setprio(3);
+                    else if (kr >= 4) __builtin_amdgcn_s_setprio(2);
+                    else if (kr >= 2) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+                one2(k, std::false_type{});
+            }
             if (!ENC) got_tag = nxt0;
         }
     } else if (tiny) {
@@ -1449,7 +1467,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     const uint64_t pn = P.pn;
                     const int hlen = P.hlen;
                     u32x4 got_tag;
-                    const u32x4 tag = gcm_packet<kNR, ENC, BPL, SUITE>(P, ks, pre.h0, rk, t1 & 3, G, sm.te, B,
+                    const u32x4 tag = gcm_packet<kNR, ENC, BPL, SUITE, WG == 512>(P, ks, pre.h0, rk, t1 & 3, G, sm.te, B,
                                                                        (uint32_t)ioff, (uint32_t)ooff, got_tag);
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
@@ -1591,6 +1609,7 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
     constexpr int SUITE = QPP_CHACHA20_POLY1305;
     const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     if (W.empty_wg) return;
+    QPP_PROBE_AT(kProbeStart);
     const uint32_t lim = W.e, planned = irange != nullptr;
     __shared__ ChachaSmem<WG> sm;
     const uint32_t t1 = threadIdx.x, p1 = W.b + ((t1 & 63) >> 2);
@@ -1649,6 +1668,7 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
         }
         last = cur;
     }
+    QPP_PROBE_AT(9);
 }
 
 // ----------------------------------------------------------- lone packets --

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../aioquic_amd/csrc/qpp_engine.hip"
@@ -19,6 +20,7 @@ static void fill(uint8_t *p, size_t n, uint32_t seed)
     }
 }
 
+#ifdef QPP_PROBE
 static void report(const char *what, const std::vector<unsigned long long> &pr)
 {
     // phases of the persistent GCM kernel (qpp_engine.hip QPP_PROBE_AT marks)
@@ -58,6 +60,19 @@ static void report(const char *what, const std::vector<unsigned long long> &pr)
         e_max = std::max(e_max, (g[kProbeEnd] - t0) / 100.0);
     }
     printf("  wave ends: first %.2f us, last %.2f us\n", e_min, e_max);
+    // start and end times as quantiles over the waves (dispatch ramp, tail)
+    std::vector<double> st, en;
+    for (int w = 0; w < kProbeWaves; ++w) {
+        const unsigned long long *g = &pr[(size_t)w * kProbeSlots];
+        if (!g[kProbeStart]) continue;
+        st.push_back((g[kProbeStart] - t0) / 100.0);
+        en.push_back((g[kProbeEnd] - t0) / 100.0);
+    }
+    std::sort(st.begin(), st.end());
+    std::sort(en.begin(), en.end());
+    auto q = [](const std::vector<double> &v, double f) { return v[(size_t)(f * (v.size() - 1))]; };
+    printf("  wave starts: q10 %.2f q50 %.2f q90 %.2f max %.2f us; ends: q10 %.2f q50 %.2f q90 %.2f us\n",
+           q(st, 0.1), q(st, 0.5), q(st, 0.9), q(st, 1.0), q(en, 0.1), q(en, 0.5), q(en, 0.9));
     // per workgroup (16 waves): its last wave's end, and the spread inside it
     double g_first = 1e30, g_last = 0, spread = 0, spread_max = 0;
     int groups = 0;
@@ -79,6 +94,7 @@ static void report(const char *what, const std::vector<unsigned long long> &pr)
     printf("  workgroup ends: first %.2f us, last %.2f us; wave-end spread inside a workgroup mean %.2f max %.2f us\n",
            g_first, g_last, spread / groups, spread_max);
 }
+#endif
 
 int main(int argc, char **argv)
 {
