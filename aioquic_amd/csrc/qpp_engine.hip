@@ -1231,6 +1231,7 @@ struct __attribute__((aligned(16))) GcmSmem {
     uint32_t eused[NE];                       // last acquisition (LRU tick)
 
     uint32_t lock, tick, next;                // entry lock; LRU clock; next item of the share
+    uint32_t exited;                          // pooled: waves past their last item
     uint32_t wslot[WG / 64];                  // per wave: the slot it is running
     uint32_t went[WG / 64];                   // per wave: that slot's table entry
 };
@@ -1347,6 +1348,20 @@ __device__ __forceinline__ qpp_desc study_desc(const qpp_desc *, uint32_t p)
 #define QPP_DESC(i) desc[i]
 #endif
 
+// Launch-wide item pool of a 1024-thread GCM launch (pool != null, a slot of
+// the key table's PoolRing): the workgroups' contiguous shares cover all but
+// the last 1/kPoolDiv of the launch's items, which any wave takes, once its
+// workgroup's share is done, from the pool's counter (pool[0]; one global
+// atomic per pooled item).  The CUs of the 8 XCDs do not run at one rate
+// (static shares ended 1313-1366 us by XCD on one box, profiles/r5ad_gcm_pool.txt),
+// so the pool lets the faster ones take the slower ones' last items.  The
+// last wave of the last workgroup (pool[1] counts workgroups out) zeroes the
+// slot for its next launch.  Single-key launches only: in a bucketed launch
+// over many keys the pooled items scatter each key over many workgroups'
+// GHASH table entries (config 4 -6 %, config 5 -0.4 %; the north star +0.4
+// to +1.6 %, profiles/r5ad_gcm_pool.txt).
+constexpr uint32_t kPoolDiv = 12;
+
 template <int SUITE, bool ENC, int WG, int BPL>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_gcm(const KeySlot *__restrict__ slots,
                                               const uint8_t *__restrict__ gtab, uint32_t cap,
@@ -1354,7 +1369,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                               const uint8_t *gin, uint8_t *gout,
                                               qpp_result *__restrict__ res,
                                               const uint32_t *__restrict__ items,
-                                              const uint32_t *__restrict__ irange)
+                                              const uint32_t *__restrict__ irange,
+                                              uint32_t *__restrict__ pool)
 {
     constexpr int kNR = SUITE == QPP_AES_256_GCM ? 14 : 10;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1367,9 +1383,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         ie = irange[2 * SUITE + 1];
     }
     const uint32_t total = ie > ib ? ie - ib : 0u;
-    const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
-    const uint32_t sb = ib + min(total, per * blockIdx.x), se = ib + min(total, per * (blockIdx.x + 1));
-    if (sb >= se) return;  // uniform over the workgroup
+    // the pooled items [ib + stat, ie) (pool: every workgroup stays to the
+    // end, which counts it out)
+    const uint32_t pool_n = pool ? total / kPoolDiv : 0u, stat = total - pool_n;
+    const uint32_t per = (stat + gridDim.x - 1) / gridDim.x;
+    const uint32_t sb = ib + min(stat, per * blockIdx.x), se = ib + min(stat, per * (blockIdx.x + 1));
+    if (!pool && sb >= se) return;  // uniform over the workgroup
     __shared__ GcmSmem<WG> sm;
     // Thread-derived values are recomputed where they are used, from the
     // wave index (an SGPR) and a fresh lane id, instead of being kept live
@@ -1387,6 +1406,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         sm.lock = 0u;
         sm.tick = 0u;
         sm.next = sb;
+        sm.exited = 0u;
     }
     if (threadIdx.x < WG / 64) sm.wslot[threadIdx.x] = kNoSlot;
     __syncthreads();
@@ -1401,7 +1421,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         uint32_t j = 0;
         if (lane_fresh() == 0) j = atomicAdd(&sm.next, 1u);
         j = __builtin_amdgcn_readfirstlane(j);
-        if (j >= se) break;
+        if (j >= se) {
+            // the share is done: the launch's pool (bounded: each grab
+            // takes a new ticket)
+            if (!pool) break;
+            uint32_t q = 0;
+            if (lane_fresh() == 0) q = atomicAdd(&pool[0], 1u);
+            q = __builtin_amdgcn_readfirstlane(q);
+            if (q >= pool_n) break;
+            j = ib + stat + q;
+        }
         QPP_PROBE_AT(1);  // the previous item's tail, the grab
         QPP_PROBE_COUNT();
         // the item's positions [wb, we) of desc
@@ -1558,6 +1587,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     if (__builtin_amdgcn_readfirstlane(lds_ld(&sm.wslot[wv])) != kNoSlot)
         tab_release<WG>(sm, __builtin_amdgcn_readfirstlane(lds_ld(&sm.went[wv])));
+    // the last wave of the last workgroup zeroes the pool for its next launch
+    // (every wave has taken its last ticket by then)
+    if (pool && lane_fresh() == 0 && atomicAdd(&sm.exited, 1u) == (uint32_t)(WG / 64 - 1) &&
+        atomicAdd(&pool[1], 1u) == gridDim.x - 1) {
+        atomicExch(&pool[0], 0u);
+        atomicExch(&pool[1], 0u);
+    }
     QPP_PROBE_AT(9);
 }
 
@@ -2403,6 +2439,23 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 
 using namespace qpp;
 
+// Item-pool slots of the persistent GCM launches (k_gcm's pool argument):
+// kPoolSlots counter pairs in device memory, one 128-byte line each, zero
+// between launches.  A launch takes a slot whose previous launch has
+// completed (its event, recorded on that launch's stream after it, has
+// fired) and which no other launch holds, so launches on different streams
+// or threads never share a slot; with none free the launch runs on static
+// shares alone (pool = null).
+constexpr int kPoolSlots = 32;
+constexpr uint32_t kPoolStride = 32;  // uint32 per slot
+struct PoolRing {
+    std::mutex mu;
+    uint32_t *d = nullptr;
+    hipEvent_t ev[kPoolSlots] = {};
+    uint8_t state[kPoolSlots] = {};  // 0 free, 1 held by a launch being enqueued, 2 event recorded
+    int next = 0;
+};
+
 struct qpp_keytab {
     uint32_t cap;
     int device;
@@ -2412,7 +2465,55 @@ struct qpp_keytab {
     uint32_t km_cap;
     uint8_t *h_suite;      // host mirror: suite of every slot (0xff = empty)
     uint32_t n_suite[3];   // installed slots per suite
+    PoolRing *pool;        // item pools of the GCM launches
 };
+
+// A free pool slot (its counters zero) or -1.
+static int pool_acquire(const qpp_keytab *kt)
+{
+    PoolRing *r = kt->pool;
+    if (!r) return -1;
+    std::lock_guard<std::mutex> l(r->mu);
+    for (int i = 0; i < kPoolSlots; ++i) {
+        const int sl = (r->next + i) % kPoolSlots;
+        if (r->state[sl] == 1) continue;
+        if (r->state[sl] == 2) {
+            const hipError_t q = hipEventQuery(r->ev[sl]);
+            if (q != hipSuccess) {
+                (void)hipGetLastError();  // still in flight (hipErrorNotReady) or failed: not reusable now
+                continue;
+            }
+        } else if (!r->ev[sl] && hipEventCreateWithFlags(&r->ev[sl], hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            r->ev[sl] = nullptr;
+            continue;
+        }
+        r->state[sl] = 1;
+        r->next = (sl + 1) % kPoolSlots;
+        return sl;
+    }
+    return -1;
+}
+
+// After the launch that held slot sl was enqueued on s (launched = it was):
+// the slot is reusable once the event recorded here fires.  A launch that
+// did not happen left the counters untouched.
+static void pool_release(const qpp_keytab *kt, int sl, hipStream_t s, bool launched)
+{
+    if (sl < 0) return;
+    PoolRing *r = kt->pool;
+    std::lock_guard<std::mutex> l(r->mu);
+    if (!launched) {
+        r->state[sl] = 0;
+        return;
+    }
+    if (hipEventRecord(r->ev[sl], s) != hipSuccess) {
+        (void)hipGetLastError();
+        r->state[sl] = 1;  // never reused: its launch may still be running
+        return;
+    }
+    r->state[sl] = 2;
+}
 
 // Host mirror of the slots' suites, so a launch goes only to the suites the
 // table holds right now (set, derive and clear keep it current).
@@ -2523,7 +2624,10 @@ int qpp_keytab_create(uint32_t capacity, qpp_keytab **out)
         return QPP_E_NOMEM;
     }
     memset(kt->h_suite, 0xff, capacity);
-    if (hipMalloc(&kt->d_slots, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
+    kt->pool = new (std::nothrow) PoolRing();
+    if (!kt->pool || hipMalloc(&kt->pool->d, (size_t)kPoolSlots * kPoolStride * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(kt->pool->d, 0, (size_t)kPoolSlots * kPoolStride * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&kt->d_slots, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
         hipMalloc(&kt->d_gtab, (size_t)capacity * (kGhashTabBytes + kGhPowBytes)) != hipSuccess ||
         hipMemset(kt->d_slots, 0xff, (size_t)capacity * sizeof(KeySlot)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
@@ -2541,6 +2645,14 @@ void qpp_keytab_destroy(qpp_keytab *kt)
     if (kt->d_slots) (void)hipFree(kt->d_slots);
     if (kt->d_gtab) (void)hipFree(kt->d_gtab);
     if (kt->d_km) (void)hipFree(kt->d_km);
+    if (kt->pool) {
+        // (the caller has completed every launch on the table before
+        // destroying it, quic_pp.h; the events go with the counters)
+        for (hipEvent_t &e : kt->pool->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (kt->pool->d) (void)hipFree(kt->pool->d);
+        delete kt->pool;
+    }
     free(kt->h_suite);
     free(kt);
 }
@@ -2797,14 +2909,19 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
 #define QPP_LAUNCH_GCM_W(SUITE, BPLV, WGV)                                                     \
     do {                                                                                       \
         const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
+        const int psl = WGV == 1024 && kt->n_suite[SUITE] == 1 ? pool_acquire(kt) : -1;        \
+        uint32_t *pl = psl >= 0 ? kt->pool->d + (size_t)psl * kPoolStride : nullptr;          \
         if (enc)                                                                               \
             hipLaunchKernelGGL((k_gcm<SUITE, true, WGV, BPLV>), grid, block, 0, s,             \
                                kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
-                               d_items, d_irange);                                             \
+                               d_items, d_irange, pl);                                         \
         else                                                                                   \
             hipLaunchKernelGGL((k_gcm<SUITE, false, WGV, BPLV>), grid, block, 0, s,            \
                                kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
-                               d_items, d_irange);                                             \
+                               d_items, d_irange, pl);                                         \
+        const hipError_t lerr = hipGetLastError();                                             \
+        pool_release(kt, psl, s, lerr == hipSuccess);                                          \
+        if (lerr != hipSuccess) return QPP_E_HIP;                                              \
     } while (0)
 #define QPP_LAUNCH_GCM_B(SUITE, BPLV)                                                          \
     do {                                                                                       \

@@ -153,6 +153,8 @@ int qpp_device_check(void);             /* QPP_OK if the current device is gfx95
  * HeaderProtection_init (_crypto.c:232-266): one device launch expands AES
  * round keys, H = E_K(0^128) and the GHASH tables for every slot in km. */
 int qpp_keytab_create(uint32_t capacity, qpp_keytab **out);
+/* Every launch that uses the table must have completed (its stream
+ * synchronized) before the table is destroyed. */
 void qpp_keytab_destroy(qpp_keytab *kt);
 uint32_t qpp_keytab_capacity(const qpp_keytab *kt);
 int qpp_keytab_set(qpp_keytab *kt, const qpp_key_material *km, uint32_t n, void *stream);

@@ -1,0 +1,64 @@
+"""The launch-wide item pool of the persistent GCM kernel (qpp_engine.hip,
+PoolRing / k_gcm's pool argument).
+
+A single-key AES-GCM launch of more than 4096 wave items (> 64 Ki packets)
+runs 1024-thread workgroups whose contiguous shares leave the last 1/12 of the
+items to a counter in one of the key table's 32 pool slots.  A slot is taken
+only when the launch that held it before has completed, and that launch's
+last workgroup zeroed it.  So launches on two streams, interleaved, more of
+them than there are slots, must each process every packet exactly once:
+every status OK and every output byte-equal to a launch run alone (which the
+oracle's whole-batch parity tests pin), and the round trip exact.
+"""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pool_slots_many_launches_two_streams():
+    import torch
+
+    from aioquic_amd import bench_data
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import PacketEngine
+
+    n = 65536 + 8192  # 4608 wave items: the 1024-thread shape
+    w = bench_data.make_workload(n, suite=0, n_keys=1, seed=0x9007, version=1)
+    eng = PacketEngine(w.n_keys)
+    eng.set_key_records(w.keys)
+    dev = torch.device("cuda")
+    d_in = torch.from_numpy(w.plain).to(dev)
+    d_desc = torch.from_numpy(w.desc.view(np.uint8)).to(dev)
+    d_udesc = torch.from_numpy(w.udesc.view(np.uint8)).to(dev)
+    ref = torch.zeros(w.wire_size, dtype=torch.uint8, device=dev)
+    ref_res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    eng.protect(d_desc, n, d_in, ref, ref_res)
+    torch.cuda.synchronize()
+    assert (ref_res.cpu().numpy().view(L.RESULT)["status"] == L.S_OK).all()
+
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    k = 4  # buffers per stream, checked as each round of 4 completes
+    wires = [[torch.empty_like(ref) for _ in range(k)] for _ in streams]
+    backs = [[torch.empty(w.plain_size, dtype=torch.uint8, device=dev) for _ in range(k)] for _ in streams]
+    res = [[torch.empty(n * 32, dtype=torch.uint8, device=dev) for _ in range(k)] for _ in streams]
+    launches = 0
+    for rnd in range(6):  # 6 x 2 streams x 4 x (protect + unprotect) = 96 pooled launches
+        for si, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                for b in range(k):
+                    wires[si][b].fill_(0xA5)
+                    backs[si][b].fill_(0x5A)
+                    eng.protect(d_desc, n, d_in, wires[si][b], res[si][b][: n * 16], stream=st)
+                    eng.unprotect(d_udesc, n, wires[si][b], backs[si][b], res[si][b][n * 16:], stream=st)
+                    launches += 2
+        torch.cuda.synchronize()
+        for si in range(len(streams)):
+            for b in range(k):
+                assert torch.equal(wires[si][b], ref), (rnd, si, b)
+                st = res[si][b].cpu().numpy().view(L.RESULT)
+                assert (st["status"] == L.S_OK).all(), (rnd, si, b)
+                back = backs[si][b].view(n, 1200)[:, :1184]
+                assert torch.equal(back, d_in.view(n, 1200)[:, :1184]), (rnd, si, b)
+    assert launches > 64

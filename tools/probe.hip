@@ -93,6 +93,29 @@ static void report(const char *what, const std::vector<unsigned long long> &pr)
     }
     printf("  workgroup ends: first %.2f us, last %.2f us; wave-end spread inside a workgroup mean %.2f max %.2f us\n",
            g_first, g_last, spread / groups, spread_max);
+    // workgroup ends by XCD (workgroups are dealt round-robin to the 8 XCDs)
+    {
+        double xs[8] = {}, xmin[8], xmax[8] = {};
+        int xn[8] = {};
+        for (int x = 0; x < 8; ++x) xmin[x] = 1e30;
+        for (int b = 0; b < kProbeWaves / 16; ++b) {
+            double hi = 0;
+            for (int w = b * 16; w < b * 16 + 16; ++w) {
+                const unsigned long long *g = &pr[(size_t)w * kProbeSlots];
+                if (g[kProbeStart]) hi = std::max(hi, (g[kProbeEnd] - t0) / 100.0);
+            }
+            if (hi == 0) continue;
+            const int x = b % 8;
+            xs[x] += hi;
+            xn[x]++;
+            xmin[x] = std::min(xmin[x], hi);
+            xmax[x] = std::max(xmax[x], hi);
+        }
+        printf("  workgroup ends by XCD (mean min max):");
+        for (int x = 0; x < 8; ++x)
+            if (xn[x]) printf(" [%d] %.0f %.0f %.0f", x, xs[x] / xn[x], xmin[x], xmax[x]);
+        printf("\n");
+    }
 }
 #endif
 
