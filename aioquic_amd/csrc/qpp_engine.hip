@@ -2495,18 +2495,15 @@ static int pool_acquire(const qpp_keytab *kt)
     return -1;
 }
 
-// After the launch that held slot sl was enqueued on s (launched = it was):
-// the slot is reusable once the event recorded here fires.  A launch that
-// did not happen left the counters untouched.
-static void pool_release(const qpp_keytab *kt, int sl, hipStream_t s, bool launched)
+// After the launch that held slot sl was enqueued on s: the slot is reusable
+// once the event recorded here fires.  (Recorded whether or not the launch
+// reported an error -- an error may predate it -- a launch that did not
+// happen leaves the counters at zero, and the event fires all the same.)
+static void pool_release(const qpp_keytab *kt, int sl, hipStream_t s)
 {
     if (sl < 0) return;
     PoolRing *r = kt->pool;
     std::lock_guard<std::mutex> l(r->mu);
-    if (!launched) {
-        r->state[sl] = 0;
-        return;
-    }
     if (hipEventRecord(r->ev[sl], s) != hipSuccess) {
         (void)hipGetLastError();
         r->state[sl] = 1;  // never reused: its launch may still be running
@@ -2919,9 +2916,7 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
             hipLaunchKernelGGL((k_gcm<SUITE, false, WGV, BPLV>), grid, block, 0, s,            \
                                kt->d_slots, kt->d_gtab, kt->cap, d_desc, n, d_in, d_out, d_res, \
                                d_items, d_irange, pl);                                         \
-        const hipError_t lerr = hipGetLastError();                                             \
-        pool_release(kt, psl, s, lerr == hipSuccess);                                          \
-        if (lerr != hipSuccess) return QPP_E_HIP;                                              \
+        pool_release(kt, psl, s);                                                              \
     } while (0)
 #define QPP_LAUNCH_GCM_B(SUITE, BPLV)                                                          \
     do {                                                                                       \
