@@ -21,6 +21,7 @@ static void fill(uint8_t *p, size_t n, uint32_t seed)
 }
 
 #ifdef QPP_PROBE
+static int g_wpg = 16;  // waves per workgroup of the probed kernel
 static void report(const char *what, const std::vector<unsigned long long> &pr)
 {
     // phases of the persistent GCM kernel (qpp_engine.hip QPP_PROBE_AT marks)
@@ -98,9 +99,9 @@ static void report(const char *what, const std::vector<unsigned long long> &pr)
         double xs[8] = {}, xmin[8], xmax[8] = {};
         int xn[8] = {};
         for (int x = 0; x < 8; ++x) xmin[x] = 1e30;
-        for (int b = 0; b < kProbeWaves / 16; ++b) {
+        for (int b = 0; b < kProbeWaves / g_wpg; ++b) {
             double hi = 0;
-            for (int w = b * 16; w < b * 16 + 16; ++w) {
+            for (int w = b * g_wpg; w < b * g_wpg + g_wpg; ++w) {
                 const unsigned long long *g = &pr[(size_t)w * kProbeSlots];
                 if (g[kProbeStart]) hi = std::max(hi, (g[kProbeEnd] - t0) / 100.0);
             }
@@ -186,6 +187,9 @@ int main(int argc, char **argv)
         return 0;
     }
     const int wg = suite == QPP_CHACHA20_POLY1305 ? kChachaWG : kGcmWG;
+#ifdef QPP_PROBE
+    g_wpg = wg / 64;
+#endif
 #ifdef QPP_PROBE
     std::vector<unsigned long long> pr((size_t)kProbeWaves * kProbeSlots);
 #endif
