@@ -22,14 +22,19 @@ KERNELS = ("k_gcm", "k_chacha", "k_packets")
 
 
 def per_launch(d, counter):
+    """Bytes per protect / unprotect call: each packet kernel's mean over its
+    dispatches, summed over the kernels one call launches (a mixed-suite call
+    runs k_gcm and k_chacha)."""
     out = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in KERNELS):
                 continue
-            enc = "true" in r["Kernel_Name"].split("(")[0]
-            out.setdefault("protect" if enc else "unprotect", []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) * 1024 for k, v in out.items()}
+            kname = r["Kernel_Name"].split("(")[0]
+            enc = "true" in kname
+            out.setdefault("protect" if enc else "unprotect", {}).setdefault(kname, []).append(
+                float(r["Counter_Value"]))
+    return {k: sum(sum(v) / len(v) for v in ks.values()) * 1024 for k, ks in out.items()}
 
 
 def main():
