@@ -62,3 +62,42 @@ def test_pool_slots_many_launches_two_streams():
                 back = backs[si][b].view(n, 1200)[:, :1184]
                 assert torch.equal(back, d_in.view(n, 1200)[:, :1184]), (rnd, si, b)
     assert launches > 64
+
+
+def test_pool_planned_single_key():
+    """A bucketed (planned) single-key launch takes the pool too: its pooled
+    items index the plan's item list.  Against an unplanned launch of the
+    same batch, whose outputs the oracle-pinned parity tests cover."""
+    import torch
+
+    from aioquic_amd import bench_data
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import PacketEngine
+
+    n = 65536 + 12288 + 77  # > 4096 wave items, a ragged last item
+    w = bench_data.make_workload(n, suite=1, n_keys=1, seed=0x9008, version=1)
+    eng = PacketEngine(w.n_keys)
+    eng.set_key_records(w.keys)
+    dev = torch.device("cuda")
+    d_in = torch.from_numpy(w.plain).to(dev)
+    d_desc = torch.from_numpy(w.desc.view(np.uint8)).to(dev)
+    d_udesc = torch.from_numpy(w.udesc.view(np.uint8)).to(dev)
+    outs, backs, ress = [], [], []
+    for planned in (False, True, True):
+        wire = torch.full((w.wire_size,), 0xA5, dtype=torch.uint8, device=dev)
+        back = torch.full((w.plain_size,), 0x5A, dtype=torch.uint8, device=dev)
+        r1 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        r2 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        eng.protect(d_desc, n, d_in, wire, r1, plan=eng.bucket(d_desc, n) if planned else None)
+        eng.unprotect(d_udesc, n, wire, back, r2, plan=eng.bucket(d_udesc, n) if planned else None)
+        outs.append(wire)
+        backs.append(back)
+        ress.append((r1, r2))
+    torch.cuda.synchronize()
+    for i in (1, 2):
+        assert torch.equal(outs[i], outs[0])
+        assert torch.equal(backs[i], backs[0])
+    for r1, r2 in ress:
+        assert (r1.cpu().numpy().view(L.RESULT)["status"] == L.S_OK).all()
+        assert (r2.cpu().numpy().view(L.RESULT)["status"] == L.S_OK).all()
+    assert torch.equal(backs[0].view(n, 1200)[:, :1184], d_in.view(n, 1200)[:, :1184])
