@@ -2468,11 +2468,21 @@ struct qpp_keytab {
     PoolRing *pool;        // item pools of the GCM launches
 };
 
+// QPP_GCM_POOL=0 (a study switch, read once per process): static shares only.
+static bool pool_choice()
+{
+    static const bool b = [] {
+        const char *v = getenv("QPP_GCM_POOL");
+        return !(v && v[0] == '0');
+    }();
+    return b;
+}
+
 // A free pool slot (its counters zero) or -1.
 static int pool_acquire(const qpp_keytab *kt)
 {
     PoolRing *r = kt->pool;
-    if (!r) return -1;
+    if (!r || !pool_choice()) return -1;
     std::lock_guard<std::mutex> l(r->mu);
     for (int i = 0; i < kPoolSlots; ++i) {
         const int sl = (r->next + i) % kPoolSlots;
