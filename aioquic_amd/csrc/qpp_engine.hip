@@ -1360,7 +1360,10 @@ __device__ __forceinline__ qpp_desc study_desc(const qpp_desc *, uint32_t p)
 // over many keys the pooled items scatter each key over many workgroups'
 // GHASH table entries (config 4 -6 %, config 5 -0.4 %; the north star +0.4
 // to +1.6 %, profiles/r5ad_gcm_pool.txt).
-constexpr uint32_t kPoolDiv = 12;
+#ifndef QPP_POOL_DIV
+#define QPP_POOL_DIV 12  // build-time study switch
+#endif
+constexpr uint32_t kPoolDiv = QPP_POOL_DIV;
 
 template <int SUITE, bool ENC, int WG, int BPL>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_gcm(const KeySlot *__restrict__ slots,
