@@ -15,6 +15,16 @@ from aioquic_amd import layout as L  # noqa: E402
 from aioquic_amd.batch import MultiDeviceEngine  # noqa: E402
 from aioquic_amd.bench_data import make_workload  # noqa: E402
 
+if os.environ.get("QPP_PROBE_INTERLEAVE") == "1":
+    # study: every page this process touches from here on interleaved over
+    # the host's NUMA nodes (set_mempolicy(MPOL_INTERLEAVE), syscall 238)
+    import ctypes
+
+    libc = ctypes.CDLL(None, use_errno=True)
+    nodes = sorted(int(d[4:]) for d in os.listdir("/sys/devices/system/node") if d.startswith("node"))
+    mask = ctypes.c_ulong(sum(1 << k for k in nodes))
+    rc = libc.syscall(238, 3, ctypes.byref(mask), ctypes.c_ulong(64))
+    print("interleave over nodes", nodes, "rc", rc, file=sys.stderr)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["staged", "registered"]  # run in this order
 w = make_workload(n, suite=0, n_keys=1, seed=0x9001, version=1)
