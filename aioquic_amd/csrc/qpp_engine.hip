@@ -2430,6 +2430,7 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
 #include <string.h>
 
 #include <algorithm>
+#include <immintrin.h>
 #include <pthread.h>
 
 #include <atomic>
@@ -3157,6 +3158,49 @@ void *qpp_session_stream(qpp_session *s) { return s ? (void *)s->stream : NULL; 
 // pool replaces a std::thread per part and copy (up to 8 x 64 thread starts
 // per 1 Mi-packet call), and a chunk's copy-out runs on it while the calling
 // thread stages the next chunks.
+// Host copies between caller memory and pinned staging with non-temporal
+// stores: a plain memcpy below glibc's non-temporal threshold reads each
+// destination line before writing it (write-allocate), so a copy moves three
+// times its size through host memory instead of two.  QPP_COPY_NT=0 (a study
+// switch, read once per process) keeps memcpy.
+static bool copy_nt_choice()
+{
+    static const bool b = [] {
+        const char *v = getenv("QPP_COPY_NT");
+        return !(v && v[0] == '0') && __builtin_cpu_supports("avx2");
+    }();
+    return b;
+}
+
+__attribute__((target("avx2"))) static void copy_nt_avx2(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    size_t head = (size_t)((32u - ((uintptr_t)dst & 31u)) & 31u);
+    if (head > n) head = n;
+    memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256((const __m256i *)(src + i));
+        const __m256i b = _mm256_loadu_si256((const __m256i *)(src + i + 32));
+        const __m256i c = _mm256_loadu_si256((const __m256i *)(src + i + 64));
+        const __m256i d = _mm256_loadu_si256((const __m256i *)(src + i + 96));
+        _mm256_stream_si256((__m256i *)(dst + i), a);
+        _mm256_stream_si256((__m256i *)(dst + i + 32), b);
+        _mm256_stream_si256((__m256i *)(dst + i + 64), c);
+        _mm256_stream_si256((__m256i *)(dst + i + 96), d);
+    }
+    memcpy(dst + i, src + i, n - i);
+    _mm_sfence();  // the streamed lines are visible before the copy is reported done
+}
+
+static void copy_bytes(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    if (n >= ((size_t)1 << 16) && copy_nt_choice()) copy_nt_avx2(dst, src, n);
+    else memcpy(dst, src, n);
+}
+
 struct CopyGroup {
     std::mutex mu;
     std::condition_variable cv;
@@ -3229,7 +3273,7 @@ class CopyPool {
                 t = q_.front();
                 q_.pop_front();
             }
-            memcpy(t.dst, t.src, t.len);
+            copy_bytes(t.dst, t.src, t.len);
             bool last;
             {
                 std::lock_guard<std::mutex> l(t.g->mu);
@@ -3254,7 +3298,7 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, CopyGroup
 {
     constexpr size_t kPart = (size_t)4 << 20;
     if (bytes < 2 * kPart) {
-        memcpy(dst, src, bytes);
+        copy_bytes(dst, src, bytes);
         return;
     }
     CopyPool &pool = CopyPool::get();
@@ -3266,7 +3310,7 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, CopyGroup
     for (size_t lo = g ? 0 : step; lo < bytes; lo += step)
         pool.submit(dst + lo, src + lo, lo + step < bytes ? step : bytes - lo, grp);
     if (!g) {
-        memcpy(dst, src, step < bytes ? step : bytes);  // the caller's own part
+        copy_bytes(dst, src, step < bytes ? step : bytes);  // the caller's own part
         local.wait();
     }
 }
