@@ -180,6 +180,12 @@ class MultiDeviceEngine:
     def unprotect_into(self, desc: np.ndarray, data: np.ndarray, out: np.ndarray, results: np.ndarray) -> None:
         _into_arrays(self.multi.unprotect_into, desc, data, out, results)
 
+    def trace(self, enable=None) -> list:
+        """Per device, the host-copy / PCIe / kernel phases of its session's
+        last traced pipelined call (qpp_multi_trace); enable=True / False turns
+        tracing on / off for the following calls."""
+        return self.multi.trace(-1 if enable is None else int(bool(enable)))
+
 
 def _into_arrays(fn, desc, data, out, results) -> None:
     desc = np.ascontiguousarray(desc, dtype=L.DESC)

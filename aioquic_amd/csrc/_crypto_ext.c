@@ -764,6 +764,37 @@ static PyObject *multi_into_py(MultiObject *self, PyObject *args, int enc)
 static PyObject *Multi_protect_into(MultiObject *self, PyObject *args) { return multi_into_py(self, args, 1); }
 static PyObject *Multi_unprotect_into(MultiObject *self, PyObject *args) { return multi_into_py(self, args, 0); }
 
+/* trace(enable=-1) -> [dict per device]: the phases of each device session's
+ * last traced pipelined call (qpp_multi_trace); enable 1 / 0 turns tracing
+ * on / off for the following calls. */
+static PyObject *Multi_trace(MultiObject *self, PyObject *args)
+{
+    int enable = -1;
+    if (!PyArg_ParseTuple(args, "|i", &enable)) return NULL;
+    qpp_trace t[16];
+    const int k = qpp_multi_trace(self->m, enable, t, 16);
+    if (k < 0) {
+        check_rc(k);
+        return NULL;
+    }
+    PyObject *lst = PyList_New(0);
+    for (int i = 0; lst && i < k; ++i) {
+        PyObject *d = Py_BuildValue(
+            "{s:I,s:I,s:d,s:d,s:d,s:d,s:d,s:d,s:d,s:d,s:d,s:d,s:d}", "pipelined", t[i].pipelined, "chunks",
+            t[i].chunks, "total_ms", t[i].total_ms, "submit_ms", t[i].submit_ms, "copy_in_ms", t[i].copy_in_ms,
+            "copy_out_ms", t[i].copy_out_ms, "wait_ms", t[i].wait_ms, "h2d_ms", t[i].h2d_ms, "kernel_ms",
+            t[i].kernel_ms, "d2h_ms", t[i].d2h_ms, "gpu_span_ms", t[i].gpu_span_ms, "in_bytes", t[i].in_bytes,
+            "out_bytes", t[i].out_bytes);
+        if (!d || PyList_Append(lst, d) < 0) {
+            Py_XDECREF(d);
+            Py_DECREF(lst);
+            return NULL;
+        }
+        Py_DECREF(d);
+    }
+    return lst;
+}
+
 static PyObject *Multi_devices(MultiObject *self, void *unused)
 {
     return PyLong_FromLong(qpp_multi_devices(self->m));
@@ -777,6 +808,8 @@ static PyMethodDef Multi_methods[] = {
      "protect_into(desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
     {"unprotect_into", (PyCFunction)Multi_unprotect_into, METH_VARARGS,
      "unprotect_into(desc_ptr, n, in_ptr, in_len, out_ptr, out_len, res_ptr)"},
+    {"trace", (PyCFunction)Multi_trace, METH_VARARGS,
+     "trace(enable=-1) -> per device, the last traced call's host / PCIe / kernel phases"},
     {NULL},
 };
 

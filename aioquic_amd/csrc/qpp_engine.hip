@@ -1217,6 +1217,11 @@ __device__ uint32_t g_qpp_watchdog;
 // spills); the host lowers both only under QPP_SPIN_LIMIT, a test switch.
 __device__ uint32_t g_qpp_spin_tab = 1u << 22;
 __device__ uint32_t g_qpp_spin_lone = 1u << 18;
+// Test switch (QPP_PAIR_DELAY): sleep rounds the second wave of a pair launch
+// spends before handing its share over, so that with QPP_SPIN_LIMIT=0 the
+// first wave gives up deterministically (tests/test_gpu_watchdog.py).  0 in
+// every product run.
+__device__ uint32_t g_qpp_pair_delay = 0u;
 
 template <int WG, int NE = gcm_tab_entries<WG>()>
 struct __attribute__((aligned(16))) GcmSmem {
@@ -1577,7 +1582,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             }
             if (fail) {
                 if (s == cur && (t & 3) == 0) {
-                    const qpp_desc d = desc[p];
+                    const qpp_desc d = QPP_DESC(p);
                     res[planned ? d.rsv : p] = qpp_result{d.pn, (uint16_t)fail, 0, 0};
                 }
                 continue;
@@ -2013,6 +2018,10 @@ __global__ __launch_bounds__(kLoneWG) void k_lone_gcm(const KeySlot *__restrict_
         bool handed = false;  // first wave: the second wave's share arrived
         if (pair) {
             if (part == 1) {
+                {
+                    const uint32_t dl = __builtin_nontemporal_load(&g_qpp_pair_delay);
+                    for (uint32_t it = 0; it < dl; ++it) __builtin_amdgcn_s_sleep(127);
+                }
                 // hand the share over (and CT blocks 0-1 in scr, if this wave
                 // wrote them); the release orders those stores before the flag
                 if (lane == 0) xch[ps] = tag;
@@ -2482,6 +2491,10 @@ static bool pool_choice()
     return b;
 }
 
+// Launches that found every pool slot held and ran on static shares alone
+// (qpp_pool_fallbacks; tests/test_gpu_pool.py).
+static std::atomic<uint64_t> g_pool_fallbacks{0};
+
 // A free pool slot (its counters zero) or -1.
 static int pool_acquire(const qpp_keytab *kt)
 {
@@ -2506,6 +2519,7 @@ static int pool_acquire(const qpp_keytab *kt)
         r->next = (sl + 1) % kPoolSlots;
         return sl;
     }
+    g_pool_fallbacks.fetch_add(1, std::memory_order_relaxed);
     return -1;
 }
 
@@ -2566,6 +2580,11 @@ struct qpp_session {
     uint8_t *d_in, *d_out, *d_misc;
     size_t misc_bytes;
     qpp_plan *plan;                  // bucketing of batches of >= kSessionPlanMin packets
+    // qpp_session_trace: timing events around every chunk's H2D, kernels and
+    // D2H (start / end), created on first enable; the last traced call
+    bool trace;
+    hipEvent_t tev[6][kPipeMaxChunks];
+    qpp_trace last;
 };
 
 // Host batches of at least this many packets are bucketed by (suite, slot)
@@ -2583,6 +2602,8 @@ constexpr uint32_t kSessionPlanMin = 128;
 extern "C" {
 
 int qpp_abi_version(void) { return QPP_ABI_VERSION; }
+
+uint64_t qpp_pool_fallbacks(void) { return g_pool_fallbacks.load(std::memory_order_relaxed); }
 
 uint32_t qpp_watchdog_count(void)
 {
@@ -2841,15 +2862,25 @@ static int apply_spin_env(hipStream_t s)
         const char *v = getenv("QPP_SPIN_LIMIT");
         return v ? atol(v) : -1L;
     }();
-    if (env < 0) return QPP_OK;
+    static const long delay = [] {
+        const char *v = getenv("QPP_PAIR_DELAY");  // test switch, g_qpp_pair_delay
+        return v ? atol(v) : -1L;
+    }();
+    if (env < 0 && delay < 0) return QPP_OK;
     static std::atomic<uint64_t> done{0};
     int dev = 0;
     (void)hipGetDevice(&dev);
     const uint64_t bit = 1ull << (dev & 63);
     if (done.load() & bit) return QPP_OK;
-    const uint32_t v = (uint32_t)env;
-    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_qpp_spin_tab), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_qpp_spin_lone), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    if (env >= 0) {
+        const uint32_t v = (uint32_t)env;
+        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_qpp_spin_tab), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_qpp_spin_lone), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    }
+    if (delay >= 0) {
+        const uint32_t v = (uint32_t)delay;
+        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_qpp_pair_delay), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
     done.fetch_or(bit);
     return QPP_OK;
@@ -3130,6 +3161,8 @@ void qpp_session_destroy(qpp_session *s)
         if (s->ev_in[c]) (void)hipEventDestroy(s->ev_in[c]);
         if (s->ev_k[c]) (void)hipEventDestroy(s->ev_k[c]);
         if (s->ev_out[c]) (void)hipEventDestroy(s->ev_out[c]);
+        for (int k = 0; k < 6; ++k)
+            if (s->tev[k][c]) (void)hipEventDestroy(s->tev[k][c]);
     }
     if (s->s_in) (void)hipStreamDestroy(s->s_in);
     if (s->s_out) (void)hipStreamDestroy(s->s_out);
@@ -3205,6 +3238,7 @@ struct CopyGroup {
     std::mutex mu;
     std::condition_variable cv;
     int pending = 0;
+    std::atomic<uint64_t> busy_ns{0};  // summed duration of the pool's tasks (qpp_trace)
     void wait()
     {
         std::unique_lock<std::mutex> l(mu);
@@ -3273,13 +3307,19 @@ class CopyPool {
                 t = q_.front();
                 q_.pop_front();
             }
+            const auto t0 = std::chrono::steady_clock::now();
             copy_bytes(t.dst, t.src, t.len);
-            bool last;
+            t.g->busy_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                       std::chrono::steady_clock::now() - t0).count(),
+                                   std::memory_order_relaxed);
             {
+                // notify while holding the group's lock: the waiter cannot see
+                // pending == 0 (and destroy the group, which lives on its
+                // stack) until this worker has released the lock, after which
+                // it never touches the group again
                 std::lock_guard<std::mutex> l(t.g->mu);
-                last = --t.g->pending == 0;
+                if (--t.g->pending == 0) t.g->cv.notify_all();
             }
-            if (last) t.g->cv.notify_all();
         }
     }
     int n_ = 8;
@@ -3298,7 +3338,12 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, CopyGroup
 {
     constexpr size_t kPart = (size_t)4 << 20;
     if (bytes < 2 * kPart) {
+        const auto t0 = std::chrono::steady_clock::now();
         copy_bytes(dst, src, bytes);
+        if (g)
+            g->busy_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                     std::chrono::steady_clock::now() - t0).count(),
+                                 std::memory_order_relaxed);
         return;
     }
     CopyPool &pool = CopyPool::get();
@@ -3358,11 +3403,6 @@ static bool trace_on()
     static const bool b = getenv("QPP_SESSION_TRACE") != nullptr;
     return b;
 }
-static double trace_now()
-{
-    if (!trace_on()) return 0.0;
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 // Chunk c of the batch: its descriptors are copied into pinned staging and
 // bounds-checked by the host, its input extent is copied into pinned staging
@@ -3386,7 +3426,12 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     qpp_desc *dd = (qpp_desc *)s->d_misc;
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
-    const double t_start = trace_now();
+    const bool tr = s->trace;
+    const auto clk = [] { return std::chrono::duration<double, std::milli>(
+                              std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_start = clk();
+    double t_copy_in = 0.0;
+    double in_bytes = 0.0, out_bytes = 0.0;
     // the caller may have assembled its input / wants its output in the
     // session's own staging (qpp_session_stage): no host copy then
     const bool in_direct = in == s->h_in, out_direct = out == s->h_out;
@@ -3430,6 +3475,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         const uint32_t a = first[c], b = first[c + 1];
         memcpy(hd + a, desc + a, (size_t)(b - a) * sizeof(qpp_desc));
         reject_out_of_bounds(enc, hd + a, b - a, in_len, out_len);
+        if (tr) HIPCHK(hipEventRecord(s->tev[0][c], s->s_in));
         if (b > a)
             HIPCHK(hipMemcpyAsync(dd + a, hd + a, (size_t)(b - a) * sizeof(qpp_desc), hipMemcpyHostToDevice,
                                   s->s_in));
@@ -3443,17 +3489,28 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         }
         if (hi > in_len) hi = in_len;
         if (lo < hi) {
-            if (!in_direct) par_memcpy(s->h_in + lo, in + lo, hi - lo);
+            if (!in_direct) {
+                const double t0 = tr ? clk() : 0.0;
+                par_memcpy(s->h_in + lo, in + lo, hi - lo);
+                if (tr) t_copy_in += clk() - t0;
+            }
             HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice, s->s_in));
+            in_bytes += (double)(hi - lo);
         }
+        in_bytes += (double)(b - a) * sizeof(qpp_desc);
         HIPCHK(hipEventRecord(s->ev_in[c], s->s_in));
+        if (tr) HIPCHK(hipEventRecord(s->tev[1][c], s->s_in));
         HIPCHK(hipStreamWaitEvent(s->stream, s->ev_in[c], 0));
+        if (tr) HIPCHK(hipEventRecord(s->tev[2][c], s->stream));
         if (b > a) {
             rc = session_launch(enc, s, kt, dd + a, b - a, dr + a);
             if (rc != QPP_OK) break;
         }
         HIPCHK(hipEventRecord(s->ev_k[c], s->stream));
+        if (tr) HIPCHK(hipEventRecord(s->tev[3][c], s->stream));
         HIPCHK(hipStreamWaitEvent(s->s_out, s->ev_k[c], 0));
+        if (tr) HIPCHK(hipEventRecord(s->tev[4][c], s->s_out));
+        out_bytes += (double)(olo[c + 1] - olo[c]) + (double)(b - a) * sizeof(qpp_result);
         if (olo[c + 1] > olo[c])
             HIPCHK(hipMemcpyAsync(s->h_out + olo[c], s->d_out + olo[c], olo[c + 1] - olo[c], hipMemcpyDeviceToHost,
                                s->s_out));
@@ -3461,6 +3518,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
             HIPCHK(hipMemcpyAsync(hr + a, dr + a, (size_t)(b - a) * sizeof(qpp_result), hipMemcpyDeviceToHost,
                                s->s_out));
         HIPCHK(hipEventRecord(s->ev_out[c], s->s_out));
+        if (tr) HIPCHK(hipEventRecord(s->tev[5][c], s->s_out));
         // hand back chunks whose D2H has already landed while later ones fly
         while (next_out < c) {
             if (hipEventQuery(s->ev_out[next_out]) != hipSuccess) {
@@ -3471,18 +3529,43 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         }
     }
     if (rc != QPP_OK) return rc;
-    const double t_sub = trace_now();
+    const double t_sub = clk();
+    const int early = next_out;
     for (int c = next_out; c < chunks; ++c) {
         HIPCHK(hipEventSynchronize(s->ev_out[c]));
         hand_back(c);
     }
     HIPCHK(hipStreamSynchronize(s->s_out));
-    if (trace_on()) {
-        outg.wait();
+    outg.wait();
+    const double t_end = clk();
+    if (tr) {
+        qpp_trace &T = s->last;
+        T = qpp_trace{};
+        T.pipelined = 1;
+        T.chunks = (uint32_t)chunks;
+        T.total_ms = t_end - t_start;
+        T.submit_ms = t_sub - t_start;
+        T.copy_in_ms = t_copy_in;
+        T.copy_out_ms = (double)outg.busy_ns.load() * 1e-6;
+        T.wait_ms = t_end - t_sub;
+        T.in_bytes = in_bytes;
+        T.out_bytes = out_bytes;
+        float ms = 0.f;
+        for (int c = 0; c < chunks; ++c) {
+            HIPCHK(hipEventElapsedTime(&ms, s->tev[0][c], s->tev[1][c]));
+            T.h2d_ms += ms;
+            HIPCHK(hipEventElapsedTime(&ms, s->tev[2][c], s->tev[3][c]));
+            T.kernel_ms += ms;
+            HIPCHK(hipEventElapsedTime(&ms, s->tev[4][c], s->tev[5][c]));
+            T.d2h_ms += ms;
+        }
+        HIPCHK(hipEventElapsedTime(&ms, s->tev[0][0], s->tev[5][chunks - 1]));
+        T.gpu_span_ms = ms;
+    }
+    if (trace_on())
         fprintf(stderr, "qpp session: %s %u packets %d chunks in %d out %d: submit %.2f ms, wait %.2f ms (%d handed back early)\n",
                 enc ? "protect" : "unprotect", n, chunks, (int)in_direct, (int)out_direct,
-                t_sub - t_start, trace_now() - t_sub, next_out);
-    }
+                t_sub - t_start, t_end - t_sub, early);
     return QPP_OK;
 }
 
@@ -3603,6 +3686,28 @@ int qpp_session_unprotect(qpp_session *s, const qpp_keytab *kt, const qpp_desc *
                           size_t out_len, qpp_result *res)
 {
     return session_drain_on_error(s, session_run(false, s, kt, desc, n, in, in_len, out, out_len, res));
+}
+
+int qpp_session_trace(qpp_session *s, int enable, qpp_trace *last)
+{
+    if (!s) return QPP_E_ARG;
+    if (last) *last = s->last;
+    if (enable > 0 && !s->tev[0][0]) {
+        for (int k = 0; k < 6; ++k)
+            for (int c = 0; c < kPipeMaxChunks; ++c)
+                if (hipEventCreate(&s->tev[k][c]) != hipSuccess) {
+                    (void)hipGetLastError();
+                    for (int k2 = 0; k2 < 6; ++k2)
+                        for (int c2 = 0; c2 < kPipeMaxChunks; ++c2) {
+                            if (s->tev[k2][c2]) (void)hipEventDestroy(s->tev[k2][c2]);
+                            s->tev[k2][c2] = nullptr;
+                        }
+                    return QPP_E_HIP;
+                }
+    }
+    if (enable >= 0) s->trace = enable > 0;
+    if (s->trace) s->last = qpp_trace{};  // a call that does not pipeline reports pipelined = 0
+    return QPP_OK;
 }
 
 int qpp_session_stage(qpp_session *s, size_t bytes, uint32_t n, uint8_t **h_in, uint8_t **h_out)
@@ -3849,6 +3954,19 @@ int qpp_multi_unprotect(qpp_multi *m, const qpp_desc *desc, uint32_t n, const ui
                         uint8_t *out, size_t out_len, qpp_result *res)
 {
     return multi_run(false, m, desc, n, in, in_len, out, out_len, res);
+}
+
+int qpp_multi_trace(qpp_multi *m, int enable, qpp_trace *last, int max)
+{
+    if (!m || max < 0 || (max > 0 && !last)) return QPP_E_ARG;
+    int prev = 0, rc = QPP_OK, k = 0;
+    (void)hipGetDevice(&prev);
+    for (; k < m->n && rc == QPP_OK; ++k) {
+        if (hipSetDevice(m->device[k]) != hipSuccess) rc = QPP_E_HIP;
+        if (rc == QPP_OK) rc = qpp_session_trace(m->s[k], enable, k < max ? last + k : nullptr);
+    }
+    (void)hipSetDevice(prev);
+    return rc == QPP_OK ? (m->n < max ? m->n : max) : rc;
 }
 
 }  // extern "C"

@@ -709,13 +709,16 @@ def L_RESULT():
     return L.RESULT
 
 
-def e2e_host_devices(cfg, seed, n, reps=3):
+def e2e_host_devices(cfg, seed, n, reps=5):
     """The library's own host-buffer path over every visible GPU
     (MultiDeviceEngine / qpp_multi: one host batch cut into contiguous ranges,
     one session and key-table replica per device, host threads in parallel):
     host memory -> protect -> host, then host -> unprotect -> host, per device
     count 1..D, from and into caller-owned pageable arrays.  PCIe-inclusive;
-    never the bench value."""
+    never the bench value.  After the timed round trips, one more round trip
+    runs with the sessions' tracing on (qpp_multi_trace: host copies in and
+    out of pinned staging, H2D, kernels, D2H per call), reported as `phases`
+    beside that round trip's own rate."""
     import torch
     from aioquic_amd.batch import MultiDeviceEngine
     from aioquic_amd.bench_data import make_workload
@@ -728,6 +731,10 @@ def e2e_host_devices(cfg, seed, n, reps=3):
     back = np.empty(w.plain_size, np.uint8)
     r1 = np.empty(n, L_RESULT())
     r2 = np.empty(n, L_RESULT())
+
+    def rnd(t):
+        return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()}
+
     for d in range(1, torch.cuda.device_count() + 1):
         eng = MultiDeviceEngine(w.n_keys, devices=list(range(d)))
         eng.set_key_records(w.keys)
@@ -741,12 +748,26 @@ def e2e_host_devices(cfg, seed, n, reps=3):
             eng.unprotect_into(w.udesc, wire, back, r2)
             times.append(time.perf_counter() - t0)
         ok = bool((r1["status"] == 0).all() and (r2["status"] == 0).all() and np.array_equal(back, plain))
-        out[str(d)] = {"gib_s": round(n * 1200 / float(np.median(times)) / GIB, 3), "round_trip_ok": ok}
+        # the traced round trip (timing events on every chunk: not in `times`)
+        eng.trace(True)
+        t0 = time.perf_counter()
+        eng.protect_into(w.desc, plain, wire, r1)
+        t_p = eng.trace()
+        eng.unprotect_into(w.udesc, wire, back, r2)
+        t_u = eng.trace()
+        t_traced = time.perf_counter() - t0
+        eng.trace(False)
+        out[str(d)] = {"gib_s": round(n * 1200 / float(np.median(times)) / GIB, 3), "round_trip_ok": ok,
+                       "samples_gib_s": [round(n * 1200 / t / GIB, 3) for t in times],
+                       "phases": {"traced_gib_s": round(n * 1200 / t_traced / GIB, 3),
+                                  "protect": [rnd(t) for t in t_p], "unprotect": [rnd(t) for t in t_u]}}
         del eng
     return {"per_device_count": out, "packets": n,
             "note": "caller-owned pageable host arrays: qpp_multi protect_into, then unprotect_into (two "
                     "synchronous calls; each a chunked pipeline: host copy into pinned staging by the library's "
-                    "copy threads, H2D, kernels, D2H, copy out)"}
+                    "copy threads, H2D, kernels, D2H, copy out); median of the timed round trips; `phases` per "
+                    "device session from one more, traced round trip (copy_in/copy_out: host copies, "
+                    "h2d/kernel/d2h: sums of the chunks' GPU durations, submit/wait: the calling thread)"}
 
 
 def e2e(eng_cls, cfg, seed, dev, n, chunks=16, n_streams=4, reps=5, mode="staged"):

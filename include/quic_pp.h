@@ -146,6 +146,11 @@ const char *qpp_source_hash(void);
  * for the packets concerned.  Never expected
  * (it would be a bug); tests check it stays 0.  A synchronous read. */
 uint32_t qpp_watchdog_count(void);
+/* Single-key AES-GCM launches (process-wide, since the library loaded) that
+ * found all of their key table's launch-pool slots held by launches still in
+ * flight and so ran without the launch-wide item pool (static shares only;
+ * the same bytes, a possibly longer tail).  Diagnostic. */
+uint64_t qpp_pool_fallbacks(void);
 const char *qpp_strerror(int rc);
 int qpp_device_check(void);             /* QPP_OK if the current device is gfx950 */
 
@@ -234,6 +239,30 @@ int qpp_session_stage(qpp_session *s, size_t bytes, uint32_t n, uint8_t **h_in, 
 int qpp_session_set_keys(qpp_session *s, qpp_keytab *kt, const qpp_key_material *km,
                          uint32_t n);
 
+/* Phases of one pipelined host-buffer call (the chunked form of
+ * qpp_session_protect / _unprotect), for a caller that wants to see where a
+ * host batch's time goes: host copies into and out of pinned staging, both
+ * PCIe directions and the kernels.  GPU phases come from timing events around
+ * every chunk's H2D, kernels and D2H (sums of the chunks' durations; the
+ * engines overlap, so they add up to more than the call). */
+typedef struct qpp_trace {
+    uint32_t pipelined;  /* 1 if the last call ran as the chunked pipeline (else the rest is 0) */
+    uint32_t chunks;
+    double total_ms;     /* the call, entry to return */
+    double submit_ms;    /* the submission loop: staging copies in, enqueues, early hand-backs */
+    double copy_in_ms;   /* caller -> pinned staging copies, wall time on the calling thread */
+    double copy_out_ms;  /* pinned staging -> caller copies, summed over the copy threads' tasks */
+    double wait_ms;      /* after the submission loop: the last chunks' D2H and copy-out */
+    double h2d_ms;       /* sum of the chunks' H2D durations (descriptors and input) */
+    double kernel_ms;    /* sum of the chunks' kernel durations */
+    double d2h_ms;       /* sum of the chunks' D2H durations (output and results) */
+    double gpu_span_ms;  /* first H2D start to last D2H end */
+    double in_bytes, out_bytes;  /* bytes sent H2D / returned D2H */
+} qpp_trace;
+/* enable != 0 turns tracing on for the session's following calls (0 off, -1
+ * unchanged); last (may be NULL) receives the previous traced call's phases. */
+int qpp_session_trace(qpp_session *s, int enable, qpp_trace *last);
+
 
 /* One host batch over several GPUs of the node (the
  * server socket of src/aioquic/asyncio/server.py:60-152 feeds all
@@ -254,6 +283,9 @@ int qpp_multi_protect(qpp_multi *m, const qpp_desc *desc, uint32_t n, const uint
                       uint8_t *out, size_t out_len, qpp_result *res);
 int qpp_multi_unprotect(qpp_multi *m, const qpp_desc *desc, uint32_t n, const uint8_t *in, size_t in_len,
                         uint8_t *out, size_t out_len, qpp_result *res);
+/* qpp_session_trace on every device's session; last[k] for device k (up to
+ * max entries).  Returns the number of devices written, or a QPP_E_* code. */
+int qpp_multi_trace(qpp_multi *m, int enable, qpp_trace *last, int max);
 
 #ifdef __cplusplus
 }

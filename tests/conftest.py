@@ -19,3 +19,14 @@ def oracle():
 
     o.lib()
     return o
+
+
+def pytest_terminal_summary(terminalreporter):
+    """State which checker each whole-batch parity test ran against (shown
+    with -q too)."""
+    mod = sys.modules.get("tests.ref_crypto")
+    if not mod or not mod.USED:
+        return
+    terminalreporter.section("whole-batch parity checkers")
+    for test_id, what in mod.USED:
+        terminalreporter.write_line(f"{test_id}: {what}")

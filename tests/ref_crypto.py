@@ -22,6 +22,17 @@ _NAMES = {0: (b"aes-128-gcm", b"aes-128-ecb", 16), 1: (b"aes-256-gcm", b"aes-256
           2: (b"chacha20-poly1305", b"chacha20", 32)}
 
 
+# Written by `make -C oracle ref` (build(), in the build container where
+# /root/reference exists) beside oracle/_ref/: it travels with the tree, so a
+# GPU box that got the marker but not the library fails the whole-batch tests
+# instead of silently checking them against the C oracle's small sample.
+EXPECTED = os.path.join(ROOT, "oracle", "_ref_expected")
+
+# (test id, checker) of every whole-batch check this session; conftest.py
+# prints them in the terminal summary, so a -q log states which checker ran
+USED = []
+
+
 def load():
     """The reference's _crypto module, or None when oracle/_ref is not built."""
     so = glob.glob(os.path.join(ROOT, "oracle", "_ref", "aioquic_ref", "_crypto*.so"))
@@ -31,6 +42,21 @@ def load():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
+
+
+def checker(test_id: str):
+    """The whole-batch checker for one test: the reference's _crypto when it
+    is built, else None (the caller's C-oracle sample).  Fails when the build
+    container built oracle/_ref (the marker is here) but the library is not,
+    and records which checker ran."""
+    ref = load()
+    if ref is None and os.path.exists(EXPECTED):
+        raise AssertionError(
+            "oracle/_ref was built from /root/reference (oracle/_ref_expected) but is missing here: "
+            "the whole-batch parity check would downgrade to the C oracle's sample")
+    USED.append((test_id, "reference _crypto (oracle/_ref), every packet both directions" if ref is not None
+                 else "C oracle (oracle/qpp_oracle.c), sample only: oracle/_ref not built"))
+    return ref
 
 
 def _objects(ref, keys):

@@ -6,6 +6,8 @@ the 1500-byte limit, tiny inputs, in-place operation, tampered tags and the
 status paths (LENGTH, NO_KEY, KEY_PHASE).  Reference: _crypto.c:115-204 and
 quic/crypto.py:75-116 through the same C ABI as the quad kernels."""
 
+import os
+
 import numpy as np
 import pytest
 
@@ -374,7 +376,7 @@ def test_lone_threshold_sizes_whole_batch(L, suite, n):
     r1, r2 = d_res.cpu().numpy().view(L.RESULT), d_res2.cpu().numpy().view(L.RESULT)
     assert (r1["status"] == 0).all() and (r2["status"] == 0).all()
     assert np.array_equal(back, w.plain)
-    ref = ref_crypto.load()
+    ref = ref_crypto.checker(os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0])
     if ref is not None:
         assert np.array_equal(ref_crypto.protect_all(ref, w), wire)
         r_back, r_pn = ref_crypto.unprotect_all(ref, w, wire)

@@ -11,8 +11,14 @@ every status OK and every output byte-equal to a launch run alone (which the
 oracle's whole-batch parity tests pin), and the round trip exact.
 """
 
+import ctypes
+import glob
+import os
+
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -38,18 +44,30 @@ def test_pool_slots_many_launches_two_streams():
     torch.cuda.synchronize()
     assert (ref_res.cpu().numpy().view(L.RESULT)["status"] == L.S_OK).all()
 
+    lib = ctypes.CDLL(glob.glob(os.path.join(ROOT, "aioquic_amd", "libquicpp.so"))[0])
+    lib.qpp_pool_fallbacks.restype = ctypes.c_uint64
+    fb0 = lib.qpp_pool_fallbacks()
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    k = 4  # buffers per stream, checked as each round of 4 completes
+    # 24 buffers per stream, every launch of a round enqueued before the round
+    # synchronizes: 96 pooled launches in flight at once, three times the
+    # ring's 32 slots, so launches find slots whose event has not fired
+    # (skipped) and rounds where every slot is held (pool = null, static
+    # shares only) -- each must still process every packet exactly once
+    k = 24
     wires = [[torch.empty_like(ref) for _ in range(k)] for _ in streams]
     backs = [[torch.empty(w.plain_size, dtype=torch.uint8, device=dev) for _ in range(k)] for _ in streams]
     res = [[torch.empty(n * 32, dtype=torch.uint8, device=dev) for _ in range(k)] for _ in streams]
     launches = 0
-    for rnd in range(6):  # 6 x 2 streams x 4 x (protect + unprotect) = 96 pooled launches
+    for rnd in range(3):  # 3 x 2 streams x 24 x (protect + unprotect) = 288 launches
         for si, st in enumerate(streams):
             with torch.cuda.stream(st):
                 for b in range(k):
                     wires[si][b].fill_(0xA5)
                     backs[si][b].fill_(0x5A)
+                    res[si][b].fill_(0xFF)
+        for b in range(k):  # the two streams' launches interleaved
+            for si, st in enumerate(streams):
+                with torch.cuda.stream(st):
                     eng.protect(d_desc, n, d_in, wires[si][b], res[si][b][: n * 16], stream=st)
                     eng.unprotect(d_udesc, n, wires[si][b], backs[si][b], res[si][b][n * 16:], stream=st)
                     launches += 2
@@ -61,7 +79,9 @@ def test_pool_slots_many_launches_two_streams():
                 assert (st["status"] == L.S_OK).all(), (rnd, si, b)
                 back = backs[si][b].view(n, 1200)[:, :1184]
                 assert torch.equal(back, d_in.view(n, 1200)[:, :1184]), (rnd, si, b)
-    assert launches > 64
+    assert launches > 3 * 32
+    # with 96 launches queued per round, some ran without a slot
+    assert lib.qpp_pool_fallbacks() > fb0
 
 
 def test_pool_planned_single_key():

@@ -51,6 +51,17 @@ def test_pair_watchdog_never_stale():
     _run_child("_pair_child", QPP_SPIN_LIMIT="0")
 
 
+def test_pair_watchdog_fires():
+    """The pair hand-over's give-up path, taken deterministically: the second
+    wave of every pair launch sleeps before handing its share over
+    (QPP_PAIR_DELAY, a test switch) while the first wave's wait is 0, so the
+    first wave always gives up (flag 0 -> 4) and the second wave finds the
+    flag taken: every packet QPP_S_INTERNAL, no plaintext on either wave, and
+    the watchdog counts the events."""
+    out = _run_child("_pair_forced_child", QPP_SPIN_LIMIT="0", QPP_PAIR_DELAY="64")
+    assert "pair forced" in out
+
+
 def _table_child():
     import torch
 
@@ -166,4 +177,55 @@ def _pair_child():
         assert ct == orc.aead_encrypt(0, key, iv, data, aad, i)
         counts["ok"] += 1
     print("pair outcomes", counts)
+    print("pair child ok")
+
+
+def _pair_forced_child():
+    from aioquic_amd import _crypto
+    from aioquic_amd import layout as L
+    from aioquic_amd._crypto import AEAD, CryptoError
+    from aioquic_amd.batch import PacketEngine, layout_packets
+    from oracle import oracle as orc
+
+    orc.lib()
+    rng = np.random.default_rng(0x9A2)
+    recs = _keys(rng, 4, (0, 1))
+    eng = PacketEngine(4)
+    eng.set_key_records(recs)
+    w0 = _crypto.watchdog_count()
+    packets = 0
+    for rep in range(12):
+        k = int(rng.integers(1, 9))  # pair launches: at most 8 packets
+        headers, payloads, pns, slots = _random_batch(rng, k, 4, recs)
+        inbuf, desc, size = layout_packets(headers, payloads, pns, slots)
+        _, res_g = eng.protect_host(desc, inbuf.tobytes(), size)
+        out_o, res_o = orc.protect_batch(recs, desc, inbuf, size)
+        ok = res_o["status"] == L.S_OK
+        assert (res_g["status"][ok] == L.S_INTERNAL).all(), (rep, res_g["status"])
+        assert (res_g["out_len"][ok] == 0).all()
+        ud = desc.copy()
+        ud["len"] = res_o["out_len"]
+        ud["hdr_len"] = [len(x) - ((x[0] & 3) + 1) for x in headers]
+        u_g, r_g = eng.unprotect_host(ud, out_o.tobytes(), size)
+        for j in range(k):
+            if not ok[j]:
+                continue
+            assert int(r_g[j]["status"]) == L.S_INTERNAL, (rep, j, int(r_g[j]["status"]))
+            # no plaintext from either wave: past the longest header up to the tag
+            o = int(ud[j]["out_off"])
+            lo, hi = o + int(ud[j]["hdr_len"]) + 4, o + int(ud[j]["len"]) - 16
+            assert not u_g[lo:hi].any(), (rep, j)
+            packets += 2
+    key, iv = rng.bytes(16), rng.bytes(12)
+    aead = AEAD(b"aes-128-gcm", key, iv)
+    for i in range(4):
+        try:
+            aead.encrypt(rng.bytes(300 + i), rng.bytes(13), i)
+        except CryptoError as e:
+            assert "Internal error" in str(e)
+        else:
+            raise AssertionError("a forced give-up returned bytes")
+    fired = _crypto.watchdog_count() - w0
+    assert fired >= packets, (fired, packets)
+    print("pair forced", packets, "packets, watchdog events", fired)
     print("pair child ok")

@@ -104,3 +104,38 @@ def test_multi_empty_middle_range_out_of_order():
     b = multi.protect_host(d, w.plain, w.wire_size)
     assert (a[1]["status"][300:600] == L.S_LENGTH).all() and (a[1]["status"][:300] == L.S_OK).all()
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_trace_reports_pipeline_phases():
+    """qpp_multi_trace / MultiDeviceEngine.trace: a host batch large enough
+    for the chunked pipeline (>= 64 MiB of output) reports its phases, and
+    tracing changes no byte.  Untraced and small calls report pipelined = 0."""
+    from aioquic_amd import bench_data
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import MultiDeviceEngine
+
+    n = 65536  # 75 MiB of wire
+    w = bench_data.make_workload(n, suite=0, n_keys=1, seed=0x54)
+    eng = MultiDeviceEngine(w.n_keys, devices=[0])
+    eng.set_key_records(w.keys)
+    wire0 = np.empty(w.wire_size, np.uint8)
+    r0 = np.empty(n, L.RESULT)
+    eng.protect_into(w.desc, w.plain, wire0, r0)
+    assert eng.trace()[0]["pipelined"] == 0  # tracing was off
+    eng.trace(True)
+    wire = np.empty(w.wire_size, np.uint8)
+    r1 = np.empty(n, L.RESULT)
+    eng.protect_into(w.desc, w.plain, wire, r1)
+    (t,) = eng.trace()
+    assert np.array_equal(wire, wire0) and np.array_equal(r1, r0)
+    assert t["pipelined"] == 1 and t["chunks"] >= 2
+    assert t["in_bytes"] >= w.plain_size and t["out_bytes"] >= w.wire_size
+    for k in ("total_ms", "submit_ms", "copy_in_ms", "copy_out_ms", "h2d_ms", "kernel_ms", "d2h_ms", "gpu_span_ms"):
+        assert t[k] > 0, (k, t)
+    assert t["total_ms"] >= t["submit_ms"] and t["gpu_span_ms"] >= max(t["h2d_ms"], t["kernel_ms"], t["d2h_ms"]) * 0.99
+    back = np.empty(w.plain_size, np.uint8)
+    r2 = np.empty(n, L.RESULT)
+    eng.unprotect_into(w.udesc, wire, back, r2)
+    assert eng.trace()[0]["pipelined"] == 1
+    assert (r2["status"] == 0).all() and np.array_equal(back, w.plain)
+    eng.trace(False)
