@@ -953,6 +953,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
 #pragma unroll
         for (int t = 0; t < 4; ++t) lds_dma16(B.in, stage + t * kChRegion, blk_off(4 * (4 * k - 1 + t) + sub));
     };
+    QPP_PROBE_AT(1);  // (probe build) descriptor, header, pkt_begin
     const uint32_t qoff = (lane_fresh() >> 2) * 64;  // the quad's 64 bytes in each region
     // the packet fields the chunk loop does not use (HP mask, packet number,
     // header layout) wait in LDS until the tag: 128 VGPRs at 4 waves per SIMD
@@ -997,7 +998,12 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
     auto chunk_io = [&](int k, int c, const uint32_t (&blk)[16], u32x4 (&x)[4]) {
         // (the DMA retires in issue order, after the previous step's stores:
         // vmcnt(0) waits for both)
+#ifdef QPP_CH_MEMPRIO
+        __builtin_amdgcn_s_setprio(QPP_CH_MEMPRIO);  // study: the memory side first
+#endif
+        QPP_PROBE_AT(4);  // (probe build) the ChaCha20 block and Poly1305 before this wait
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        QPP_PROBE_AT(5);  // the wait for this step's input (and the last step's stores)
         uint8_t *mine = stage + sub * kChRegion + qoff;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -1027,6 +1033,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
+        QPP_PROBE_AT(6);  // (probe build) xor through LDS
         // coalesced stores of the quad's full blocks: instruction t, lane j ->
         // block j of chunk 4k - 1 + t
 #pragma unroll
@@ -1040,7 +1047,12 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         // Poly1305 and the next ChaCha20 block)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
+        QPP_PROBE_AT(8);  // (probe build) the stores' reads and issue
         if (k + 1 < steps) dma(k + 1);
+#ifdef QPP_CH_MEMPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+        QPP_PROBE_AT(3);  // (probe build) next step's DMA issue
     };
 
     // step 0: unit `sub` (lane 0: the one-time key, lanes 1-3: chunks 0-2)
@@ -1088,6 +1100,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
                 acc = p130_mul(p130_add(acc, p130_block(a)), (g == n_a - 1 && 3 < chunks) ? r13 : r);
             }
         }
+        QPP_PROBE_AT(2);  // key block, powers, associated data
         chunk_io(0, sub - 1, blk, x);
     }
     // step k: the ChaCha20 block of unit 4k + sub beside Poly1305 of the
@@ -1107,6 +1120,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         chunk_io(k, c, blk, x);
     }
     poly(x, 4 * (steps - 1) + sub - 1);
+    QPP_PROBE_AT(4);
     {
         const uint8_t *src = P.src;
         uint8_t *dst = P.dst;
@@ -1160,6 +1174,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
             wipe_payload(P, sub, [&](int i) { return ((i >> 2) + 1) & 3; });
         }
     }
+    QPP_PROBE_AT(7);  // close, tag, header protection
 }
 
 template <bool ENC>
@@ -1369,6 +1384,12 @@ __device__ __forceinline__ qpp_desc study_desc(const qpp_desc *, uint32_t p)
 #define QPP_POOL_DIV 12  // build-time study switch
 #endif
 constexpr uint32_t kPoolDiv = QPP_POOL_DIV;
+#ifndef QPP_POOL512
+#define QPP_POOL512 0  // study switch: the item pool for the 512-thread shape too
+#endif
+#ifndef QPP_PRIO512
+#define QPP_PRIO512 1  // study switch: issue priority by progress in the 512-thread shape
+#endif
 
 template <int SUITE, bool ENC, int WG, int BPL>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_gcm(const KeySlot *__restrict__ slots,
@@ -1504,7 +1525,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     const uint64_t pn = P.pn;
                     const int hlen = P.hlen;
                     u32x4 got_tag;
-                    const u32x4 tag = gcm_packet<kNR, ENC, BPL, SUITE, WG == 512>(P, ks, pre.h0, rk, t1 & 3, G, sm.te, B,
+                    const u32x4 tag = gcm_packet<kNR, ENC, BPL, SUITE, WG == 512 && QPP_PRIO512>(P, ks, pre.h0, rk, t1 & 3, G, sm.te, B,
                                                                        (uint32_t)ioff, (uint32_t)ooff, got_tag);
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
@@ -1653,6 +1674,13 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
     constexpr int SUITE = QPP_CHACHA20_POLY1305;
     const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     if (W.empty_wg) return;
+#ifdef QPP_CH_STAGGER
+    {
+        // study: waves start QPP_CH_STAGGER x 64 cycles apart by their slot in the SIMD
+        const uint32_t slot = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (3 << 11));
+        for (uint32_t i = 0; i < slot * QPP_CH_STAGGER; ++i) __builtin_amdgcn_s_sleep(1);
+    }
+#endif
     QPP_PROBE_AT(kProbeStart);
     const uint32_t lim = W.e, planned = irange != nullptr;
     __shared__ ChachaSmem<WG> sm;
@@ -2921,9 +2949,12 @@ static uint32_t gcm_grid(uint32_t items, uint32_t waves_per_wg)
 // single-key launch, its waves drawing pooled chunks of 8 items from a
 // launch-wide counter fetched ahead of need, measured no faster than one of
 // 1024 at the north star, profiles/r4f_ab_pooled.txt.)
+#ifndef QPP_TWO_WG_ITEMS
+#define QPP_TWO_WG_ITEMS 16u  // study switch: items per CU up to which the 512 shape runs
+#endif
 static bool gcm_two_wg(const qpp_keytab *kt, uint32_t suite, uint32_t items)
 {
-    return kt->n_suite[suite] == 1 && items <= cu_count() * 16u;  // 2 workgroups x 8 waves per CU
+    return kt->n_suite[suite] == 1 && items <= cu_count() * (uint32_t)QPP_TWO_WG_ITEMS;  // 2 workgroups x 8 waves per CU
 }
 
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
@@ -2951,7 +2982,7 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
 #define QPP_LAUNCH_GCM_W(SUITE, BPLV, WGV)                                                     \
     do {                                                                                       \
         const dim3 grid(gcm_grid(waves, WGV / 64)), block(WGV);                                 \
-        const int psl = WGV == 1024 && kt->n_suite[SUITE] == 1 ? pool_acquire(kt) : -1;        \
+        const int psl = (WGV == 1024 || QPP_POOL512) && kt->n_suite[SUITE] == 1 ? pool_acquire(kt) : -1; \
         uint32_t *pl = psl >= 0 ? kt->pool->d + (size_t)psl * kPoolStride : nullptr;          \
         if (enc)                                                                               \
             hipLaunchKernelGGL((k_gcm<SUITE, true, WGV, BPLV>), grid, block, 0, s,             \
@@ -3434,7 +3465,15 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     double in_bytes = 0.0, out_bytes = 0.0;
     // the caller may have assembled its input / wants its output in the
     // session's own staging (qpp_session_stage): no host copy then
-    const bool in_direct = in == s->h_in, out_direct = out == s->h_out;
+    // QPP_STUDY_NOCOPY=in|out|both (a timing study, read once per process;
+    // wrong output by design): skip the host copies into / out of staging, to
+    // measure the PCIe legs without the copies' host-memory traffic
+    static const int nocopy = [] {
+        const char *v = getenv("QPP_STUDY_NOCOPY");
+        if (!v) return 0;
+        return (strstr(v, "in") || strstr(v, "both") ? 1 : 0) | (strstr(v, "out") || strstr(v, "both") ? 2 : 0);
+    }();
+    const bool in_direct = in == s->h_in || (nocopy & 1), out_direct = out == s->h_out || (nocopy & 2);
     HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     size_t olo[kPipeMaxChunks + 1];
     uint32_t first[kPipeMaxChunks + 1];

@@ -22,13 +22,19 @@ static void fill(uint8_t *p, size_t n, uint32_t seed)
 
 #ifdef QPP_PROBE
 static int g_wpg = 16;  // waves per workgroup of the probed kernel
+static bool g_chacha = false;
 static void report(const char *what, const std::vector<unsigned long long> &pr)
 {
     // phases of the persistent GCM kernel (qpp_engine.hip QPP_PROBE_AT marks)
-    const char *names[] = {"prologue (AES image, entry init, sync)", "item tail + grab", "table entry (acquire)",
+    static const char *gcm_names[] = {"prologue (AES image, entry init, sync)", "item tail + grab", "table entry (acquire)",
                            "descriptor, pkt_begin, park", "AAD fold + counter cache", "step loop",
                            "closing GHASH multiply (global tables)", "finish: tail, tag, header, result",
                            "release", "exit"};
+    static const char *chacha_names[] = {"-", "descriptor, header, pkt_begin", "key block, r powers, AAD",
+                           "next step's DMA issue", "ChaCha20 block + Poly1305 (compute)",
+                           "wait: step input DMA (+ last stores)", "xor via LDS (ds_read, xor, ds_write)",
+                           "close, tag, HP, result", "stores (LDS reads, buffer stores)", "exit"};
+    const char **names = g_chacha ? chacha_names : gcm_names;
     constexpr int NP = 10;
     int waves = 0;
     unsigned long long t0 = ~0ull, t1 = 0, items = 0;
@@ -189,6 +195,7 @@ int main(int argc, char **argv)
     const int wg = suite == QPP_CHACHA20_POLY1305 ? kChachaWG : kGcmWG;
 #ifdef QPP_PROBE
     g_wpg = wg / 64;
+    g_chacha = suite == QPP_CHACHA20_POLY1305;
 #endif
 #ifdef QPP_PROBE
     std::vector<unsigned long long> pr((size_t)kProbeWaves * kProbeSlots);
