@@ -2459,6 +2459,37 @@ __global__ void k_clear_slots(KeySlot *slots, const uint32_t *idx, uint32_t n, u
     if (i < n && idx[i] < cap) slots[idx[i]].suite = 0xffu;
 }
 
+// PCIe copies by the GPU's own loads and stores (qpp_session's D2H legs, and
+// H2D under QPP_H2D_KERNEL): range y of the launch copies n_y bytes from src_y
+// to dst_y, one of them a pinned host buffer's device view, in 16-byte
+// non-temporal accesses (D2H: posted PCIe writes; bytes at a range's unaligned
+// ends one by one).  The runtime's D2H
+// on the copy engines ran at 27-30 GB/s in some processes on these boxes and
+// 56-57 GB/s in others, while this kernel ran at 53-54 GB/s in every one
+// (tools/d2h_probe.hip, profiles/r6_host_path/d2h_probe.txt).
+typedef unsigned int xfer_v4 __attribute__((ext_vector_type(4)));
+constexpr int kXferWG = 256;
+__global__ __launch_bounds__(kXferWG) void k_xfer(const uint8_t *__restrict__ s0, uint8_t *d0, size_t n0,
+                                                const uint8_t *__restrict__ s1, uint8_t *d1, size_t n1)
+{
+    const uint8_t *src = blockIdx.y ? s1 : s0;
+    uint8_t *dst = blockIdx.y ? d1 : d0;
+    const size_t n = blockIdx.y ? n1 : n0;
+    const size_t tid = (size_t)blockIdx.x * kXferWG + threadIdx.x, step = (size_t)gridDim.x * kXferWG;
+    if ((((uintptr_t)src ^ (uintptr_t)dst) & 15) != 0) {  // never in the session (same offsets)
+        for (size_t i = tid; i < n; i += step) dst[i] = src[i];
+        return;
+    }
+    size_t head = (16 - ((uintptr_t)src & 15)) & 15;
+    if (head > n) head = n;
+    const size_t body = (n - head) >> 4, tail = n - head - 16 * body;
+    if (tid < head) dst[tid] = src[tid];
+    const xfer_v4 *s16 = (const xfer_v4 *)(src + head);
+    xfer_v4 *d16 = (xfer_v4 *)(dst + head);
+    for (size_t i = tid; i < body; i += step) __builtin_nontemporal_store(__builtin_nontemporal_load(&s16[i]), &d16[i]);
+    if (tid < tail) dst[head + 16 * body + tid] = src[head + 16 * body + tid];
+}
+
 }  // namespace qpp
 
 // ======================================================== host: C ABI ======
@@ -3427,6 +3458,54 @@ static int session_launch(bool enc, qpp_session *s, const qpp_keytab *kt, const 
     return rc;
 }
 
+// D2H of a session: up to two device ranges into pinned host memory (device
+// views), by k_xfer.  QPP_D2H_KERNEL=0 (a study switch, read once per
+// process) uses hipMemcpyAsync on the stream instead.
+static bool d2h_kernel_choice()
+{
+    static const bool b = [] {
+        const char *v = getenv("QPP_D2H_KERNEL");
+        return !(v && v[0] == '0');
+    }();
+    return b;
+}
+
+static int launch_xfer(uint8_t *d0, const uint8_t *s0, size_t n0, uint8_t *d1, const uint8_t *s1, size_t n1,
+                       hipStream_t st)
+{
+    if (!n0 && !n1) return QPP_OK;
+    const size_t units = (std::max(n0, n1) + 15) / 16;
+    // ~8 16-byte units per thread, at most 1024 workgroups per range
+    size_t g = (units + (size_t)kXferWG * 8 - 1) / ((size_t)kXferWG * 8);
+    if (g < 1) g = 1;
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_xfer, dim3((uint32_t)g, n1 ? 2u : 1u), dim3(kXferWG), 0, st, s0, d0, n0, s1, d1, n1);
+    HIPCHK(hipGetLastError());
+    return QPP_OK;
+}
+
+static int session_d2h(uint8_t *h0, uint8_t *hd0, const uint8_t *s0, size_t n0, uint8_t *h1, uint8_t *hd1,
+                       const uint8_t *s1, size_t n1, hipStream_t st)
+{
+    if (!d2h_kernel_choice()) {
+        if (n0) HIPCHK(hipMemcpyAsync(h0, s0, n0, hipMemcpyDeviceToHost, st));
+        if (n1) HIPCHK(hipMemcpyAsync(h1, s1, n1, hipMemcpyDeviceToHost, st));
+        return QPP_OK;
+    }
+    return launch_xfer(hd0, s0, n0, hd1, s1, n1, st);
+}
+
+// QPP_H2D_KERNEL=1 (a study switch, read once per process): the pipelined
+// session's H2D legs by k_xfer too (default: hipMemcpyAsync, the copy engines)
+static bool h2d_kernel_choice()
+{
+    static const bool b = [] {
+        const char *v = getenv("QPP_H2D_KERNEL");
+        return v && v[0] == '1';
+    }();
+    return b;
+}
+
 // QPP_SESSION_TRACE=1: one stderr line per pipelined call with its host
 // phases (a study switch, read once per process)
 static bool trace_on()
@@ -3457,6 +3536,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     qpp_result *hr = (qpp_result *)(s->h_misc + (size_t)s->max_packets * sizeof(qpp_desc));
     qpp_desc *dd = (qpp_desc *)s->d_misc;
     qpp_result *dr = (qpp_result *)(s->d_misc + (size_t)s->max_packets * sizeof(qpp_desc));
+    qpp_result *hrd = (qpp_result *)(s->hd_misc + (size_t)s->max_packets * sizeof(qpp_desc));  // hr's device view
     const bool tr = s->trace;
     const auto clk = [] { return std::chrono::duration<double, std::milli>(
                               std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -3515,7 +3595,8 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         memcpy(hd + a, desc + a, (size_t)(b - a) * sizeof(qpp_desc));
         reject_out_of_bounds(enc, hd + a, b - a, in_len, out_len);
         if (tr) HIPCHK(hipEventRecord(s->tev[0][c], s->s_in));
-        if (b > a)
+        const bool h2dk = h2d_kernel_choice();
+        if (b > a && !h2dk)
             HIPCHK(hipMemcpyAsync(dd + a, hd + a, (size_t)(b - a) * sizeof(qpp_desc), hipMemcpyHostToDevice,
                                   s->s_in));
         size_t lo = SIZE_MAX, hi = 0;
@@ -3533,8 +3614,14 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
                 par_memcpy(s->h_in + lo, in + lo, hi - lo);
                 if (tr) t_copy_in += clk() - t0;
             }
-            HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice, s->s_in));
+            if (!h2dk) HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice, s->s_in));
             in_bytes += (double)(hi - lo);
+        }
+        if (h2dk) {
+            rc = launch_xfer((uint8_t *)(dd + a), s->hd_misc + (size_t)a * sizeof(qpp_desc),
+                             (size_t)(b - a) * sizeof(qpp_desc), lo < hi ? s->d_in + lo : nullptr,
+                             lo < hi ? s->hd_in + lo : nullptr, lo < hi ? hi - lo : 0, s->s_in);
+            if (rc != QPP_OK) break;
         }
         in_bytes += (double)(b - a) * sizeof(qpp_desc);
         HIPCHK(hipEventRecord(s->ev_in[c], s->s_in));
@@ -3550,12 +3637,13 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
         HIPCHK(hipStreamWaitEvent(s->s_out, s->ev_k[c], 0));
         if (tr) HIPCHK(hipEventRecord(s->tev[4][c], s->s_out));
         out_bytes += (double)(olo[c + 1] - olo[c]) + (double)(b - a) * sizeof(qpp_result);
-        if (olo[c + 1] > olo[c])
-            HIPCHK(hipMemcpyAsync(s->h_out + olo[c], s->d_out + olo[c], olo[c + 1] - olo[c], hipMemcpyDeviceToHost,
-                               s->s_out));
-        if (b > a)
-            HIPCHK(hipMemcpyAsync(hr + a, dr + a, (size_t)(b - a) * sizeof(qpp_result), hipMemcpyDeviceToHost,
-                               s->s_out));
+        {
+            const size_t tl = olo[c + 1] > olo[c] ? olo[c + 1] - olo[c] : 0;
+            const size_t rl = (size_t)(b - a) * sizeof(qpp_result);
+            rc = session_d2h(s->h_out + olo[c], s->hd_out + olo[c], s->d_out + olo[c], tl, (uint8_t *)(hr + a),
+                             (uint8_t *)(hrd + a), (const uint8_t *)(dr + a), rl, s->s_out);
+            if (rc != QPP_OK) break;
+        }
         HIPCHK(hipEventRecord(s->ev_out[c], s->s_out));
         if (tr) HIPCHK(hipEventRecord(s->tev[5][c], s->s_out));
         // hand back chunks whose D2H has already landed while later ones fly
@@ -3705,8 +3793,10 @@ static int session_run(bool enc, qpp_session *s, const qpp_keytab *kt, const qpp
     if (out_len) HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     rc = session_launch(enc, s, kt, dd, n, dr);
     if (rc != QPP_OK) return rc;
-    if (out_len) HIPCHK(hipMemcpyAsync(s->h_out, s->d_out, out_len, hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(hipMemcpyAsync(hr, dr, (size_t)n * sizeof(qpp_result), hipMemcpyDeviceToHost, s->stream));
+    rc = session_d2h(s->h_out, s->hd_out, s->d_out, out_len, (uint8_t *)hr,
+                     s->hd_misc + (size_t)s->max_packets * sizeof(qpp_desc), (const uint8_t *)dr,
+                     (size_t)n * sizeof(qpp_result), s->stream);
+    if (rc != QPP_OK) return rc;
     HIPCHK(hipStreamSynchronize(s->stream));
     if (out_len && out != s->h_out) memcpy(out, s->h_out, out_len);
     memcpy(res, hr, (size_t)n * sizeof(qpp_result));
