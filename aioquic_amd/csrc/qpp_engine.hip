@@ -3592,13 +3592,14 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     int next_out = 0;
     for (int c = 0; c < chunks; ++c) {
         const uint32_t a = first[c], b = first[c + 1];
+        hipStream_t sin = s->s_in;
         memcpy(hd + a, desc + a, (size_t)(b - a) * sizeof(qpp_desc));
         reject_out_of_bounds(enc, hd + a, b - a, in_len, out_len);
-        if (tr) HIPCHK(hipEventRecord(s->tev[0][c], s->s_in));
+        if (tr) HIPCHK(hipEventRecord(s->tev[0][c], sin));
         const bool h2dk = h2d_kernel_choice();
         if (b > a && !h2dk)
             HIPCHK(hipMemcpyAsync(dd + a, hd + a, (size_t)(b - a) * sizeof(qpp_desc), hipMemcpyHostToDevice,
-                                  s->s_in));
+                                  sin));
         size_t lo = SIZE_MAX, hi = 0;
         for (uint32_t i = a; i < b; ++i) {
             if (hd[i].flags & kFlagReject) continue;
@@ -3614,18 +3615,18 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
                 par_memcpy(s->h_in + lo, in + lo, hi - lo);
                 if (tr) t_copy_in += clk() - t0;
             }
-            if (!h2dk) HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice, s->s_in));
+            if (!h2dk) HIPCHK(hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice, sin));
             in_bytes += (double)(hi - lo);
         }
         if (h2dk) {
             rc = launch_xfer((uint8_t *)(dd + a), s->hd_misc + (size_t)a * sizeof(qpp_desc),
                              (size_t)(b - a) * sizeof(qpp_desc), lo < hi ? s->d_in + lo : nullptr,
-                             lo < hi ? s->hd_in + lo : nullptr, lo < hi ? hi - lo : 0, s->s_in);
+                             lo < hi ? s->hd_in + lo : nullptr, lo < hi ? hi - lo : 0, sin);
             if (rc != QPP_OK) break;
         }
         in_bytes += (double)(b - a) * sizeof(qpp_desc);
-        HIPCHK(hipEventRecord(s->ev_in[c], s->s_in));
-        if (tr) HIPCHK(hipEventRecord(s->tev[1][c], s->s_in));
+        HIPCHK(hipEventRecord(s->ev_in[c], sin));
+        if (tr) HIPCHK(hipEventRecord(s->tev[1][c], sin));
         HIPCHK(hipStreamWaitEvent(s->stream, s->ev_in[c], 0));
         if (tr) HIPCHK(hipEventRecord(s->tev[2][c], s->stream));
         if (b > a) {
