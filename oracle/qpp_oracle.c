@@ -475,20 +475,30 @@ long qo_protect(int suite, const uint8_t *key, const uint8_t iv[12], const uint8
 /* CryptoContext.decrypt_packet (quic/crypto.py:75-103), without the key-phase
  * switch: the caller passes the key it wants used.  Returns the payload length
  * or a negative QO_E_* code; fills header (out), payload (out + *hdr_len). */
-long qo_unprotect(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp_key,
-                  const uint8_t *pkt, size_t len, size_t pn_off, uint64_t expected_pn,
-                  uint8_t *out, size_t *hdr_len, uint64_t *pn)
+/* rfc_pn != 0: the truncated number decodes unsigned (RFC 9000 App. A.3, the
+ * algorithm of packet.py:118-132 without the int32 hand-over of _crypto.c:349),
+ * as the product's QPP_F_RFC_PN flag asks (include/quic_pp.h) */
+long qo_unprotect_ex(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp_key,
+                     const uint8_t *pkt, size_t len, size_t pn_off, uint64_t expected_pn,
+                     uint8_t *out, size_t *hdr_len, uint64_t *pn, int rfc_pn)
 {
     uint32_t trunc;
     int h = qo_hp_remove(suite, hp_key, pkt, len, pn_off, out, &trunc);
     if (h < 0) return QO_E_LENGTH;
     int pn_len = (out[0] & 3) + 1;
-    *pn = qo_decode_pn(qo_pn_trunc_as_int(trunc), pn_len * 8, expected_pn);
+    *pn = qo_decode_pn(rfc_pn ? (int64_t)trunc : qo_pn_trunc_as_int(trunc), pn_len * 8, expected_pn);
     *hdr_len = (size_t)h;
     long r = qo_aead_decrypt(suite, key, iv, pkt + h, len - h, out, (size_t)h, *pn, out + h);
     if (r == -1) return QO_E_LENGTH;
     if (r == -2) return QO_E_DECRYPT;
     return r;
+}
+
+long qo_unprotect(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp_key,
+                  const uint8_t *pkt, size_t len, size_t pn_off, uint64_t expected_pn,
+                  uint8_t *out, size_t *hdr_len, uint64_t *pn)
+{
+    return qo_unprotect_ex(suite, key, iv, hp_key, pkt, len, pn_off, expected_pn, out, hdr_len, pn, 0);
 }
 
 /* ------------------------------------------------------------ batch forms -- */
@@ -560,15 +570,16 @@ void qo_unprotect_batch(const qpp_key_material *keys, uint32_t n_keys, const qpp
             }
             if (!(hdr[0] & 0x80) && ((hdr[0] >> 2) & 1) != k->key_phase) {
                 int pn_len = (hdr[0] & 3) + 1;
-                r->pn = qo_decode_pn(qo_pn_trunc_as_int(trunc), 8 * pn_len, d->pn);
+                r->pn = qo_decode_pn((d->flags & QPP_F_RFC_PN) ? (int64_t)trunc : qo_pn_trunc_as_int(trunc),
+                                     8 * pn_len, d->pn);
                 r->hdr_len = (uint16_t)(d->hdr_len + pn_len);
                 r->status = QPP_S_KEY_PHASE;
                 continue;
             }
             size_t hl;
             uint64_t pn;
-            m = qo_unprotect(k->suite, k->key, k->iv, k->hp, p, d->len, d->hdr_len, d->pn, o, &hl,
-                             &pn);
+            m = qo_unprotect_ex(k->suite, k->key, k->iv, k->hp, p, d->len, d->hdr_len, d->pn, o, &hl,
+                                &pn, (d->flags & QPP_F_RFC_PN) != 0);
             r->pn = pn;
             r->hdr_len = (uint16_t)hl;
             if (m >= 0) m += (long)hl;

@@ -41,6 +41,9 @@ long qo_protect(int suite, const uint8_t *key, const uint8_t iv[12], const uint8
 long qo_unprotect(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp_key,
                   const uint8_t *pkt, size_t len, size_t pn_off, uint64_t expected_pn,
                   uint8_t *out, size_t *hdr_len, uint64_t *pn);
+long qo_unprotect_ex(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp_key,
+                     const uint8_t *pkt, size_t len, size_t pn_off, uint64_t expected_pn,
+                     uint8_t *out, size_t *hdr_len, uint64_t *pn, int rfc_pn);
 
 /* Batch forms over the product's descriptor layout (include/quic_pp.h), so a
  * test can run the oracle and the GPU on byte-identical inputs.  keys is
