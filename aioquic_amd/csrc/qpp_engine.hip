@@ -3475,10 +3475,15 @@ static int launch_xfer(uint8_t *d0, const uint8_t *s0, size_t n0, uint8_t *d1, c
 {
     if (!n0 && !n1) return QPP_OK;
     const size_t units = (std::max(n0, n1) + 15) / 16;
-    // ~8 16-byte units per thread, at most 1024 workgroups per range
+    // ~8 16-byte units per thread, at most xfer_wgs() workgroups per range
+    static const size_t cap = [] {
+        const char *v = getenv("QPP_XFER_WGS");  // study switch, read once per process
+        const long c = v ? atol(v) : 1024;
+        return (size_t)(c < 1 ? 1 : c > 4096 ? 4096 : c);
+    }();
     size_t g = (units + (size_t)kXferWG * 8 - 1) / ((size_t)kXferWG * 8);
     if (g < 1) g = 1;
-    if (g > 1024) g = 1024;
+    if (g > cap) g = cap;
     hipLaunchKernelGGL(k_xfer, dim3((uint32_t)g, n1 ? 2u : 1u), dim3(kXferWG), 0, st, s0, d0, n0, s1, d1, n1);
     HIPCHK(hipGetLastError());
     return QPP_OK;
