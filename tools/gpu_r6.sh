@@ -2,7 +2,7 @@
 # Round-6 GPU pass: parity tests, smoke, the driver's default bench command
 # (with the traced host-path round trip), optionally a rocprofv3 kernel trace
 # of the default bench and every config.
-#   gpurun -- bash tools/gpu_r6.sh TAG [tests-only|skip-tests] [prof] [sweep]
+#   gpurun -- bash tools/gpu_r6.sh TAG [all|tests-only|skip-tests] [prof] [sweep] [rehearse8]
 set -uo pipefail
 TAG=${1:-r6}
 MODE=${2:-all}
@@ -29,6 +29,10 @@ for a in "${@:3}"; do
   fi
   if [ "$a" = "sweep" ]; then
     bash tools/gpu_sweep.sh $TAG || exit 1
+  fi
+  if [ "$a" = "rehearse8" ]; then
+    timeout -k 10 400 python -u bench.py --gpus 8 --rehearse --packets 131072 --cpu-seconds 2 --cpu-all-cores 0 --no-e2e > $O/rehearsal8_$TAG.json 2> $O/rehearsal8_$TAG.err || { echo rehearsal failed; tail $O/rehearsal8_$TAG.err; exit 1; }
+    tail -c 600 $O/rehearsal8_$TAG.json
   fi
 done
 echo gpu_r6-done $TAG
