@@ -3550,15 +3550,7 @@ static int session_run_pipelined(bool enc, qpp_session *s, const qpp_keytab *kt,
     double in_bytes = 0.0, out_bytes = 0.0;
     // the caller may have assembled its input / wants its output in the
     // session's own staging (qpp_session_stage): no host copy then
-    // QPP_STUDY_NOCOPY=in|out|both (a timing study, read once per process;
-    // wrong output by design): skip the host copies into / out of staging, to
-    // measure the PCIe legs without the copies' host-memory traffic
-    static const int nocopy = [] {
-        const char *v = getenv("QPP_STUDY_NOCOPY");
-        if (!v) return 0;
-        return (strstr(v, "in") || strstr(v, "both") ? 1 : 0) | (strstr(v, "out") || strstr(v, "both") ? 2 : 0);
-    }();
-    const bool in_direct = in == s->h_in || (nocopy & 1), out_direct = out == s->h_out || (nocopy & 2);
+    const bool in_direct = in == s->h_in, out_direct = out == s->h_out;
     HIPCHK(hipMemsetAsync(s->d_out, 0, out_len, s->stream));
     size_t olo[kPipeMaxChunks + 1];
     uint32_t first[kPipeMaxChunks + 1];

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 6: the host-buffer path's phase trace at several copy-thread counts,
-# and with the host copies skipped (QPP_STUDY_NOCOPY: timing only).
+# Round 6: the host-buffer path's phase trace at several copy-thread counts
+# (NOCOPY=...: the r6i study build's QPP_STUDY_NOCOPY switch, which skipped the
+# host copies for timing and has since been removed from the library).
 set -uo pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r6h}
