@@ -139,3 +139,37 @@ def test_trace_reports_pipeline_phases():
     assert eng.trace()[0]["pipelined"] == 1
     assert (r2["status"] == 0).all() and np.array_equal(back, w.plain)
     eng.trace(False)
+
+
+def test_multi_pipelined_ranges_equal_one_session():
+    """Large host batches split over two sessions (the one-GPU stand-in for two
+    devices): each range is big enough for its session's chunked pipeline
+    (D2H legs by k_xfer), the two run at once on their own threads, and the
+    bytes and results equal one session's, both directions."""
+    from aioquic_amd import bench_data
+    from aioquic_amd import layout as L
+    from aioquic_amd.batch import MultiDeviceEngine
+
+    n = 160000  # 2 x ~96 MB of wire: both ranges pipelined
+    w = bench_data.make_workload(n, suite=0, n_keys=3, seed=0x55, mixed=(0, 2))
+    one = MultiDeviceEngine(w.n_keys, devices=[0])
+    two = MultiDeviceEngine(w.n_keys, devices=[0, 0])
+    for e in (one, two):
+        e.set_key_records(w.keys)
+    two.trace(True)
+    outs = []
+    for e in (one, two):
+        wire = np.empty(w.wire_size, np.uint8)
+        r1 = np.empty(n, L.RESULT)
+        e.protect_into(w.desc, w.plain, wire, r1)
+        back = np.empty(w.plain_size, np.uint8)
+        r2 = np.empty(n, L.RESULT)
+        e.unprotect_into(w.udesc, wire, back, r2)
+        outs.append((wire, r1, back, r2))
+    assert [t["pipelined"] for t in two.trace()] == [1, 1]
+    two.trace(False)
+    (w1, a1, b1, c1), (w2, a2, b2, c2) = outs
+    assert np.array_equal(w1, w2) and a1.tobytes() == a2.tobytes()
+    assert np.array_equal(b1, b2) and c1.tobytes() == c2.tobytes()
+    assert (a2["status"] == L.S_OK).all() and (c2["status"] == L.S_OK).all()
+    assert np.array_equal(b2, w.plain)
