@@ -486,6 +486,26 @@ __device__ __forceinline__ u32x4 aes_ctr(const CtrCache &c, uint32_t cb, const u
     return aes_rounds<NR, 3, true>(v, rk, T);
 }
 
+// Study switch (QPP_LDS_PRIO = n > 0, default 0: no instructions): issue
+// priority n while a wave issues a phase's lookups and 0 while it mixes their
+// results (QPP_LDS_PRIO_INV: the other way round), so that the waves about to
+// feed the LDS array win the SIMD's issue slots over waves doing VALU work.
+#ifndef QPP_LDS_PRIO
+#define QPP_LDS_PRIO 0
+#endif
+#ifndef QPP_LDS_PRIO_INV
+#define QPP_LDS_PRIO_INV 0
+#endif
+__device__ __forceinline__ void lds_phase_prio(bool issuing)
+{
+    if constexpr (QPP_LDS_PRIO > 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (issuing != (QPP_LDS_PRIO_INV != 0)) __builtin_amdgcn_s_setprio(QPP_LDS_PRIO);
+        else __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Two counter blocks of one packet (cb0, cb1) as one chain of LDS phases:
 // every phase issues both blocks' lookups (32 for a full round) before the
 // first use, so a block pays half the LDS round trips of aes_ctr.
@@ -493,6 +513,7 @@ template <int NR, class TE>
 __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32_t cb1,
                                          const uint32_t *rk, const TE &T, u32x4 &o0, u32x4 &o1)
 {
+    lds_phase_prio(true);
     const uint32_t x0 = T.t3(rk[3] ^ (cb0 << 24)), x1 = T.t3(rk[3] ^ (cb1 << 24));
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t u0 = c.c0 ^ x0, u1 = c.c0 ^ x1;
@@ -505,6 +526,7 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32
     for (int r = 3; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
         uint32_t e[2][16];
+        lds_phase_prio(true);
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
 #pragma unroll
@@ -516,6 +538,7 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32
             }
         }
         __builtin_amdgcn_sched_barrier(0);
+        lds_phase_prio(false);
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
 #pragma unroll
@@ -526,6 +549,7 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32
     }
     const uint32_t *k = rk + 4 * NR;
     uint32_t f[2][16];
+    lds_phase_prio(true);
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
 #pragma unroll
@@ -537,6 +561,7 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &c, uint32_t cb0, uint32
         }
     }
     __builtin_amdgcn_sched_barrier(0);
+    lds_phase_prio(false);
     uint32_t o[2][4];
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
