@@ -925,7 +925,7 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t *
 // chunks (r per block, r^12 across the other 3 lanes' chunks), lane 0 starting
 // with the associated data, and one quad sum at the end.  B / ioff / ooff:
 // the wave's buffer views and the packet's offsets in them.
-template <bool ENC>
+template <bool ENC, bool PRIO>
 __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, uint8_t *stage, uint32_t *pw,
                               const Bufs &B, uint32_t ioff, uint32_t ooff)
 {
@@ -1107,6 +1107,17 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
     // lane's previous chunk (software-pipelined by one step)
 #pragma unroll 1
     for (int k = 1; k < steps; ++k) {
+        if constexpr (PRIO) {
+            // waves further from the packet's end issue first (the sequencer
+            // arbitrates by priority, then age), so a launch of one wave per
+            // slot progresses together instead of oldest first, as k_gcm's
+            // 512-thread shape does
+            const int kr = __builtin_amdgcn_readfirstlane(steps - k);
+            if (kr >= 4) __builtin_amdgcn_s_setprio(3);
+            else if (kr == 3) __builtin_amdgcn_s_setprio(2);
+            else if (kr == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const int c = 4 * k + sub - 1;
         uint32_t blk[16];
         // the previous chunk's 4 Poly1305 blocks after double rounds 1, 3, 5, 7
@@ -1661,7 +1672,7 @@ __device__ __forceinline__ WaveSpan wave_span(uint32_t n, const uint32_t *items,
 
 // ChaCha20-Poly1305: no tables, so every wave runs its packets slot by slot
 // on its own, with the keys read from the slot (scalar loads).
-template <bool ENC, int WG>
+template <bool ENC, int WG, bool PRIO>
 __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__restrict__ slots,
                                                              uint32_t cap,
                                                              const qpp_desc *__restrict__ desc,
@@ -1682,6 +1693,7 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
     }
 #endif
     QPP_PROBE_AT(kProbeStart);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // set-up and key block: every wave at the top
     const uint32_t lim = W.e, planned = irange != nullptr;
     __shared__ ChachaSmem<WG> sm;
     const uint32_t t1 = threadIdx.x, p1 = W.b + ((t1 & 63) >> 2);
@@ -1733,7 +1745,7 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
                 const Bufs B{
                     __builtin_amdgcn_make_buffer_rsrc((void *)(gin + bi), 0, (int)kBufBytes, 0x00020000),
                     __builtin_amdgcn_make_buffer_rsrc((void *)(gout + bo), 0, (int)kBufBytes, 0x00020000)};
-                chacha_packet<ENC>(P, ks, tf & 3, sm.scratch[tf >> 2], sm.stage[tf >> 6], sm.pw[tf >> 2], B, (uint32_t)ioff,
+                chacha_packet<ENC, PRIO>(P, ks, tf & 3, sm.scratch[tf >> 2], sm.stage[tf >> 6], sm.pw[tf >> 2], B, (uint32_t)ioff,
                                    (uint32_t)ooff);
             }
             write_result<ENC>(res, planned ? desc[p1].rsv : p1, lane_fresh() & 3, P);
@@ -2988,6 +3000,19 @@ static bool gcm_two_wg(const qpp_keytab *kt, uint32_t suite, uint32_t items)
     return kt->n_suite[suite] == 1 && items <= cu_count() * (uint32_t)QPP_TWO_WG_ITEMS;  // 2 workgroups x 8 waves per CU
 }
 
+// ChaCha20-Poly1305 issue priority by progress (k_chacha PRIO): for launches
+// whose waves all fit the chip at once (kChachaWpe per SIMD, one round), so
+// each SIMD's waves end together instead of oldest first.  QPP_CHACHA_PRIO=0
+// turns it off, =2 forces it on for every launch (A/B switches, read once).
+static bool chacha_prio(uint32_t waves)
+{
+    static const int m = [] {
+        const char *v = getenv("QPP_CHACHA_PRIO");
+        return v ? atoi(v) : 1;
+    }();
+    return m == 2 || (m == 1 && waves <= cu_count() * 4u * kChachaWpe);
+}
+
 static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc, uint32_t n,
                           const uint8_t *d_in, uint8_t *d_out, qpp_result *d_res, void *stream,
                           const qpp_plan *plan = nullptr, const LoneStage *stage = nullptr)
@@ -3058,12 +3083,20 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
         HIPCHK(hipGetLastError());
     } else if (mask & (1u << QPP_CHACHA20_POLY1305)) {
         const dim3 grid((waves + kChachaWG / 64 - 1) / (kChachaWG / 64)), block(kChachaWG);
-        if (enc)
-            hipLaunchKernelGGL((k_chacha<true, kChachaWG>), grid, block, 0, s, kt->d_slots, kt->cap,
+        if (chacha_prio(waves)) {
+            if (enc)
+                hipLaunchKernelGGL((k_chacha<true, kChachaWG, true>), grid, block, 0, s, kt->d_slots, kt->cap,
+                                   d_desc, n, d_in, d_out, d_res, d_items, d_irange);
+            else
+                hipLaunchKernelGGL((k_chacha<false, kChachaWG, true>), grid, block, 0, s, kt->d_slots, kt->cap,
+                                   d_desc, n, d_in, d_out, d_res, d_items, d_irange);
+        } else if (enc) {
+            hipLaunchKernelGGL((k_chacha<true, kChachaWG, false>), grid, block, 0, s, kt->d_slots, kt->cap,
                                d_desc, n, d_in, d_out, d_res, d_items, d_irange);
-        else
-            hipLaunchKernelGGL((k_chacha<false, kChachaWG>), grid, block, 0, s, kt->d_slots, kt->cap,
+        } else {
+            hipLaunchKernelGGL((k_chacha<false, kChachaWG, false>), grid, block, 0, s, kt->d_slots, kt->cap,
                                d_desc, n, d_in, d_out, d_res, d_items, d_irange);
+        }
         HIPCHK(hipGetLastError());
     }
 #undef QPP_LAUNCH_GCM
