@@ -150,6 +150,37 @@ __device__ __forceinline__ P130 p130_mul(P130 h, P130 r)
     return P130{{o0, o1, o2, o3, o4}};
 }
 
+// d += h * r: the five 64-bit column sums of p130_mul without its carry.  A
+// sum of four such products stays below 2^64 for h limbs < 2^27 and r limbs
+// < 2^26 + 2^11 (each column < 2^57.7 per product), so four blocks of a chunk
+// can be multiplied by their own powers of r and carried once (p130_carry).
+__device__ __forceinline__ void p130_mac(uint64_t (&d)[5], P130 h, P130 r)
+{
+    const uint32_t r0 = r.v[0], r1 = r.v[1], r2 = r.v[2], r3 = r.v[3], r4 = r.v[4];
+    const uint32_t s1 = r1 * 5, s2 = r2 * 5, s3 = r3 * 5, s4 = r4 * 5;
+    const uint64_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4];
+    d[0] += h0 * r0 + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
+    d[1] += h0 * r1 + h1 * r0 + h2 * s4 + h3 * s3 + h4 * s2;
+    d[2] += h0 * r2 + h1 * r1 + h2 * r0 + h3 * s4 + h4 * s3;
+    d[3] += h0 * r3 + h1 * r2 + h2 * r1 + h3 * r0 + h4 * s4;
+    d[4] += h0 * r4 + h1 * r3 + h2 * r2 + h3 * r1 + h4 * r0;
+}
+
+// the partial carry of p130_mul on column sums (limbs < 2^26 but limb 1)
+__device__ __forceinline__ P130 p130_carry(uint64_t d0, uint64_t d1, uint64_t d2, uint64_t d3, uint64_t d4)
+{
+    d1 += d0 >> 26;
+    d2 += d1 >> 26;
+    d3 += d2 >> 26;
+    d4 += d3 >> 26;
+    uint32_t o0 = (uint32_t)d0 & kM26, o1 = (uint32_t)d1 & kM26, o2 = (uint32_t)d2 & kM26;
+    uint32_t o3 = (uint32_t)d3 & kM26, o4 = (uint32_t)d4 & kM26;
+    uint64_t c = (d4 >> 26) * 5 + o0;
+    o0 = (uint32_t)c & kM26;
+    o1 += (uint32_t)(c >> 26);
+    return P130{{o0, o1, o2, o3, o4}};
+}
+
 // clamp(r) from the first 16 bytes of the one-time key (RFC 8439 sec. 2.5)
 __device__ __forceinline__ P130 p130_r(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3)
 {

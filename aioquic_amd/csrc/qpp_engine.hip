@@ -60,8 +60,14 @@ constexpr int kChachaWpe = 4;
 constexpr int kChRegion = 64 * 16 + 16;
 constexpr int kChStage = 4 * kChRegion;
 
-// pw entries: 1, r, r^2 .. r^5, r^8
-constexpr int kPwOne = 0, kPw1 = 1, kPw8 = 6, kPwEntries = 7;
+// pw entries: 1, r, r^2 .. r^5, r^8, r^13 .. r^16
+#ifndef QPP_CH_POLY4
+#define QPP_CH_POLY4 1  // study switch: 0 = one Horner multiply (and carry) per Poly1305 block
+#endif
+#ifndef QPP_CH_CARRY_AT
+#define QPP_CH_CARRY_AT 7  // study switch: the double round after which the chunk sum is carried
+#endif
+constexpr int kPwOne = 0, kPw1 = 1, kPw8 = 6, kPw13 = 7, kPwEntries = QPP_CH_POLY4 ? 11 : 7;
 
 template <int WG>
 struct __attribute__((aligned(16))) ChachaSmem {
@@ -971,6 +977,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
     // the block's independent quarter rounds.  Blocks that do not exist
     // (c < 0: the key unit; past the payload's end) multiply by one and add
     // zero, which leaves the chain as it is.
+#if !QPP_CH_POLY4
     auto poly_blk = [&](const u32x4 (&x)[4], int c, int b) {
         {
             const int i = 4 * c + b;
@@ -988,10 +995,50 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
             acc = p130_mul(a, f);
         }
     };
+#endif
+#if QPP_CH_POLY4
+    // The chunk as one sum: the lane's chain moves by
+    //   acc <- (acc + x0) r^e0 + x1 r^e1 + x2 r^e2 + x3 r^e3,
+    // e = 16 .. 13 when the lane has a later chunk (its Horner steps r, r, r
+    // and the r^13 jump over the other lanes' chunks, multiplied out), else
+    // the chunk's own valid blocks nbv - b .. 1 (a block past the payload
+    // adds zero; no chunk at all: acc r^0).  Four independent products from
+    // the pw powers into 64-bit column sums (part b after double round 2b + 1)
+    // and one carry after the rounds, instead of four dependent multiplies
+    // each with its carry and selects.
+    uint64_t dsum[5];
+    auto poly_part = [&](const u32x4 (&x)[4], int c, int b) {
+        const bool inc = c >= 0 && c < chunks;
+        const int nbv = min(4, n_c - 4 * c);  // the chunk's blocks (fewer in the final chunk only)
+        const bool valid = inc && b < nbv;
+        const int e = !inc ? 0 : (c + 4 < chunks) ? 16 - b : valid ? nbv - b : 0;
+        const int idx = e < 13 ? e : e - (13 - kPw13);
+        P130 m = p130_block(x[b]);
+        // (x[b] is zero for a block that does not exist: only the 2^128
+        // bit of p130_block needs masking)
+        m.v[4] = valid ? m.v[4] : 0u;
+        if (b == 0) m = p130_add(m, acc);
+        P130 rp;
+#pragma unroll
+        for (int l = 0; l < 5; ++l) rp.v[l] = pw[5 * idx + l];
+        if (b == 0) {
+#pragma unroll
+            for (int l = 0; l < 5; ++l) dsum[l] = 0;
+        }
+        p130_mac(dsum, m, rp);
+    };
+    auto poly_carry = [&]() { acc = p130_carry(dsum[0], dsum[1], dsum[2], dsum[3], dsum[4]); };
+    auto poly = [&](const u32x4 (&x)[4], int c) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) poly_part(x, c, b);
+        poly_carry();
+    };
+#else
     auto poly = [&](const u32x4 (&x)[4], int c) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) poly_blk(x, c, b);
     };
+#endif
     // the memory side of step k: the lane's chunk c from region `sub` xor
     // its keystream, back through LDS to 4 coalesced stores, the next step's
     // LDS-DMA; x = the chunk's Poly1305 inputs
@@ -1075,6 +1122,19 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         const P130 b58 = p130_mul(r4, sub == 0 ? r : r4);
         const P130 r5 = p130_from_lane<0>(b58), r8 = p130_from_lane<1>(b58);
         r13 = p130_mul(r8, r5);
+#if QPP_CH_POLY4
+        {
+            // the chunk sums' powers r^13 .. r^16, one multiply per lane:
+            // lane 0 r^13 r, lane 1 r^8 r^8, lane 2 r^13 r^2, lane 3 r^13
+            const P130 one = P130{{1u, 0u, 0u, 0u, 0u}};
+            const P130 pa = sub == 1 ? r8 : r13;
+            const P130 pb = sub == 0 ? r : sub == 1 ? r8 : sub == 2 ? r2 : one;
+            const P130 pr = p130_mul(pa, pb);
+            const int slot = kPw13 + (sub == 0 ? 1 : sub == 1 ? 3 : sub == 2 ? 2 : 0);
+#pragma unroll
+            for (int l = 0; l < 5; ++l) pw[5 * slot + l] = pr.v[l];
+        }
+#endif
         if (sub == 0) {  // the close's powers (kPwOne .. kPw8)
 #pragma unroll
             for (int l = 0; l < 5; ++l) {
@@ -1121,9 +1181,18 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         const int c = 4 * k + sub - 1;
         uint32_t blk[16];
         // the previous chunk's 4 Poly1305 blocks after double rounds 1, 3, 5, 7
+#if QPP_CH_POLY4
+        // the previous chunk's 4 Poly1305 products after double rounds 1, 3,
+        // 5, 7, its carry after the last
+        chacha_block_beside(key, (uint32_t)(c + 1), n0, n1, n2, blk, [&](int i) {
+            if (i & 1 && i < 8) poly_part(x, c - 4, i >> 1);
+            if (i == QPP_CH_CARRY_AT) poly_carry();
+        });
+#else
         chacha_block_beside(key, (uint32_t)(c + 1), n0, n1, n2, blk, [&](int i) {
             if (i & 1 && i < 8) poly_blk(x, c - 4, i >> 1);
         });
+#endif
         // pin the chain here: otherwise the compiler sinks this Poly1305 step
         // to the next iteration's top (beside the loop's exit test), out of
         // the rounds' basic block
