@@ -393,7 +393,13 @@ __device__ __forceinline__ void wipe_payload(const Pkt &P, int sub, OWN own)
 {
     uint8_t *o = P.dst + P.hlen;
     for (int i = 0; 16 * i < P.clen; ++i)
-        if (own(i) == sub) st_part(o + 16 * i, u32x4{0, 0, 0, 0}, min(16, P.clen - 16 * i));
+        if (own(i) == sub) {
+            // made here: a zero the compiler hoists to the kernel's entry is
+            // held (or spilled) across everything before this rare path
+            u32x4 z = {0, 0, 0, 0};
+            asm volatile("" : "+v"(z));
+            st_part(o + 16 * i, z, min(16, P.clen - 16 * i));
+        }
 }
 
 // Buffer descriptors over the whole input / output buffers.  Offsets at or
@@ -1765,7 +1771,11 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // set-up and key block: every wave at the top
     const uint32_t lim = W.e, planned = irange != nullptr;
     __shared__ ChachaSmem<WG> sm;
-    const uint32_t t1 = threadIdx.x, p1 = W.b + ((t1 & 63) >> 2);
+    // the lane's packet and quad lane, re-derived from a fresh lane id where
+    // used (held across the slot loop, the thread id is spilled at 128 VGPRs)
+    auto p_now = [&]() -> uint32_t { return W.b + (lane_fresh() >> 2); };
+    auto sub_now = [&]() -> uint32_t { return lane_fresh() & 3; };
+    const uint32_t p1 = p_now();
     // 32-bit buffer views based at the wave's lowest input / output offsets
     // (a wave's packets must lie within 4 GiB of each other, as for GCM)
     uint64_t bi, bo;
@@ -1775,7 +1785,7 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
             const qpp_desc d = desc[p1];
             in0 = d.in_off;
             out0 = d.out_off;
-            if (d.slot >= cap && (t1 & 3) == 0) res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+            if (d.slot >= cap && sub_now() == 0) res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
         }
         bi = wave_min_u64(in0);
         bo = wave_min_u64(out0);
@@ -1787,17 +1797,18 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
     uint32_t last = kNoSlot;
     #pragma unroll 1
     for (int guard = 0; guard < 17; ++guard) {
-        const uint32_t s = p1 < lim ? desc[p1].slot : kNoSlot;
+        const uint32_t pl = p_now();
+        const uint32_t s = pl < lim ? desc[pl].slot : kNoSlot;
         const uint32_t cur = wave_min_u32(s < cap && (last == kNoSlot || s > last) ? s : kNoSlot);
         if (cur == kNoSlot) break;
         const KeySlot *ks = slots + cur;
         const uint32_t suite = ks->suite;
-        if (s == cur && suite > QPP_CHACHA20_POLY1305 && (t1 & 3) == 0) {
-            const qpp_desc d = desc[p1];
-            res[planned ? d.rsv : p1] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
+        if (s == cur && suite > QPP_CHACHA20_POLY1305 && sub_now() == 0) {
+            const qpp_desc d = desc[pl];
+            res[planned ? d.rsv : pl] = qpp_result{d.pn, QPP_S_NO_KEY, 0, 0};
         }
         if (s == cur && suite == SUITE) {
-            const qpp_desc d = desc[p1];
+            const qpp_desc d = desc[pl];
             const HdrPre pre = prefetch_hdr<ENC>(d, gin, true);
             const ConstTe T;
             Pkt P = pkt_begin<ENC, SUITE>(d, pre, gin, gout, ks, T);
@@ -1817,7 +1828,8 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
                 chacha_packet<ENC, PRIO>(P, ks, tf & 3, sm.scratch[tf >> 2], sm.stage[tf >> 6], sm.pw[tf >> 2], B, (uint32_t)ioff,
                                    (uint32_t)ooff);
             }
-            write_result<ENC>(res, planned ? desc[p1].rsv : p1, lane_fresh() & 3, P);
+            const uint32_t pr = p_now();
+            write_result<ENC>(res, planned ? desc[pr].rsv : pr, lane_fresh() & 3, P);
         }
         last = cur;
     }
