@@ -64,6 +64,9 @@ constexpr int kChStage = 4 * kChRegion;
 #ifndef QPP_CH_POLY4
 #define QPP_CH_POLY4 1  // study switch: 0 = one Horner multiply (and carry) per Poly1305 block
 #endif
+#ifndef QPP_CH_DIRECT_ST
+#define QPP_CH_DIRECT_ST 0  // study switch: 1 = each lane stores its own blocks (no LDS round trip back)
+#endif
 #ifndef QPP_CH_CARRY_AT
 #define QPP_CH_CARRY_AT 7  // study switch: the double round after which the chunk sum is carried
 #endif
@@ -1082,8 +1085,25 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
                 }
             }
             if (valid && ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[b];
+#if QPP_CH_DIRECT_ST
+            {
+                // the lane's own full block straight out (a quad's 4 stores
+                // of one instruction are 64 B apart; the 4 instructions
+                // complete the quad's 256 B)
+                const uint32_t so = (valid && nb >= 16 && !tiny) ? ooff + (uint32_t)(P.hlen + 16 * i) : kOob;
+                __builtin_amdgcn_raw_buffer_store_b128(o, B.out, (int)so, 0, 0);
+            }
+#else
             *(u32x4 *)(mine + 16 * b) = o;
+#endif
         }
+#if QPP_CH_DIRECT_ST
+        // the xor consumed every lane's input: the regions are free for the
+        // next step's DMA
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        QPP_PROBE_AT(6);  // (probe build) xor and stores
+#else
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         QPP_PROBE_AT(6);  // (probe build) xor through LDS
@@ -1101,6 +1121,7 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         QPP_PROBE_AT(8);  // (probe build) the stores' reads and issue
+#endif
         if (k + 1 < steps) dma(k + 1);
 #ifdef QPP_CH_MEMPRIO
         __builtin_amdgcn_s_setprio(0);
