@@ -87,6 +87,9 @@ def parse():
                     help="bracket the kernels of every N-th timed step (steps N-1, 2N-1, ...) with HIP "
                          "events (1 = all, the default: the kernels' event intervals then lie inside the "
                          "timed steps, so they sum to at most ms_per_step)")
+    ap.add_argument("--sustain-seconds", type=float, default=4.0,
+                    help="after the timed region (N = 1, rank 0): the same step back to back for about this "
+                         "long, reported as `sustained` (steady-state clocks; never `value`; 0 = skip)")
     ap.add_argument("--e2e", dest="e2e", action="store_true", default=True,
                     help="time pinned H2D->kernels->D2H after the timed region (the default)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false", help="skip the end-to-end leg")
@@ -602,6 +605,24 @@ def main():
     hev_flags = hev.flags
     hev.close()
 
+    # sustained: the same step back to back for a few seconds after the timed
+    # region, no events (the clocks' steady state; reported beside `value`,
+    # never as it); its last step's results are checked below like the
+    # timed region's
+    sustained = None
+    if world == 1 and args.sustain_seconds > 0:
+        k_s = max(1, int(args.sustain_seconds / max(elapsed / args.steps, 1e-6)))
+        torch.cuda.synchronize(dev)
+        t_s = time.perf_counter()
+        for _ in range(k_s):
+            step()
+        torch.cuda.synchronize(dev)
+        dt_s = time.perf_counter() - t_s
+        sustained = {"steps": k_s, "seconds": round(dt_s, 3),
+                     "gib_s": round(float(n) * 1200 * k_s / dt_s / GIB, 3),
+                     "ms_per_step": round(dt_s / k_s * 1e3, 4),
+                     "note": "the timed region's step repeated back to back after it, without timing events"}
+
     # after timing: every packet of the last step authenticated, and (unless
     # --no-check) the unprotected bytes equal the plaintext, every byte
     r1 = d_r1.cpu().numpy().view(L.RESULT)
@@ -668,6 +689,7 @@ def main():
                          "compute_floor": floor},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "sustained": sustained,
             "status_ok": ok,
             "round_trip_checked": bool(args.check),
             "ranks": per_rank,
