@@ -2954,7 +2954,10 @@ int qpp_keytab_clear(qpp_keytab *kt, const uint32_t *slots, uint32_t n, void *st
 // persistent workgroup per CU, 4 waves per SIMD), ChaCha20-Poly1305 256.
 static const int kGcmWG = 1024;
 
-static const int kChachaWG = 256;
+#ifndef QPP_CHACHA_WG
+#define QPP_CHACHA_WG 256  // study switch: the ChaCha20-Poly1305 kernel's workgroup size
+#endif
+static const int kChachaWG = QPP_CHACHA_WG;
 
 // GCM blocks per lane per step (gcm_pad): 2 (r2i, same box: north star
 // 1.419 -> 1.389 ms protect, config 4 310 -> 316 GiB/s; WRITE_SIZE 2.08 ->
