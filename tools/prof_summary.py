@@ -38,9 +38,10 @@ def bench_line(d):
 
 def timed_launches(d, out_csv=None):
     """Per kernel, the dispatches of the bench's K timed steps only (the
-    first W steps are warm-up at a lower clock): each step launches every
-    kernel the same number of times, so the timed ones are the last
-    K x (calls / (W + K)) dispatches of each kernel in dispatch order."""
+    first W steps are warm-up at a lower clock, and an N = 1 line's
+    `sustained` steps follow the timed ones): each step launches every
+    kernel the same number of times, so the timed ones are dispatches
+    W x per .. (W + K) x per of each kernel in dispatch order."""
     b = bench_line(d)
     traces = glob.glob(os.path.join(d, "kt", "*kernel_trace.csv"))
     if not b or not traces:
@@ -51,12 +52,14 @@ def timed_launches(d, out_csv=None):
     for r in rows:
         by[short(r["Kernel_Name"])].append(r)
     steps, warm = int(b["steps"]), int(b["warmup"])
+    extra = int((b.get("sustained") or {}).get("steps", 0))
+    total = steps + warm + extra
     keep = {}
     for k, rs in by.items():
-        if len(rs) % (steps + warm):
+        if len(rs) % total:
             continue  # not a per-step kernel (setup, copies, the HBM copy probe)
-        per = len(rs) // (steps + warm)
-        keep[k] = rs[len(rs) - steps * per:]
+        per = len(rs) // total
+        keep[k] = rs[warm * per:(warm + steps) * per]
     if out_csv:
         kept = sorted((r for rs in keep.values() for r in rs), key=lambda r: int(r["Start_Timestamp"]))
         with open(out_csv, "w", newline="") as f:
