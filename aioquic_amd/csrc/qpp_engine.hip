@@ -1494,6 +1494,9 @@ constexpr uint32_t kPoolDiv = QPP_POOL_DIV;
 #ifndef QPP_POOL512
 #define QPP_POOL512 0  // study switch: the item pool for the 512-thread shape too
 #endif
+#ifndef QPP_SHARE_PRIO
+#define QPP_SHARE_PRIO 0  // study switch: 512-thread shape, issue priority by the workgroup's share left
+#endif
 #ifndef QPP_PRIO512
 #define QPP_PRIO512 1  // study switch: issue priority by progress in the 512-thread shape
 #endif
@@ -1567,6 +1570,19 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             if (q >= pool_n) break;
             j = ib + stat + q;
         }
+#if QPP_SHARE_PRIO
+        if constexpr (WG == 512) {
+            // the two workgroups of a CU progress through their shares
+            // together: the one with more of its share left issues first
+            // (pooled items, at the launch's end, at the bottom)
+            const uint32_t tot = se - sb, rem = j < se ? se - j : 0u;
+            const uint32_t pr = tot ? min(3u, (4u * rem) / (tot + 1u)) : 0u;
+            if (pr >= 3) __builtin_amdgcn_s_setprio(3);
+            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         QPP_PROBE_AT(1);  // the previous item's tail, the grab
         QPP_PROBE_COUNT();
         // the item's positions [wb, we) of desc
