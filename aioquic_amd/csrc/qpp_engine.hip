@@ -612,7 +612,7 @@ template <int NR, bool ENC, int BPL, int SUITE, bool PRIO>
 __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, const u32x4 h0,
                                             const uint32_t *rk, int sub, const GhashTabs &G,
                                             const uint8_t *te, const Bufs &B, uint32_t ioff, uint32_t ooff,
-                                            u32x4 &got_tag)
+                                            u32x4 &got_tag, uint32_t pbase = 0u)
 {
     const LdsTe T{te, (lane_fresh() & 31) * 4};
     const int hlen = P.hlen, clen = P.clen;
@@ -798,10 +798,20 @@ __device__ __forceinline__ u32x4 gcm_packet(const Pkt &P, const KeySlot *ks, con
                     // persistent 1024-thread workgroups, for every item or
                     // only each share's last ones, no gain at 1 Mi)
                     const int kr = __builtin_amdgcn_readfirstlane(k);
+#if QPP_COMBO_PRIO
+                    // study: the workgroup's share level (pbase 0 or 2) plus
+                    // one for the item's first half
+                    const uint32_t lv = __builtin_amdgcn_readfirstlane(pbase) + (kr >= 5 ? 1u : 0u);
+                    if (lv >= 3) __builtin_amdgcn_s_setprio(3);
+                    else if (lv == 2) __builtin_amdgcn_s_setprio(2);
+                    else if (lv == 1) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+#else
                     if (kr >= 7) __builtin_amdgcn_s_setprio(3);
                     else if (kr >= 4) __builtin_amdgcn_s_setprio(2);
                     else if (kr >= 2) __builtin_amdgcn_s_setprio(1);
                     else __builtin_amdgcn_s_setprio(0);
+#endif
                 }
                 one2(k, std::false_type{});
             }
@@ -1494,6 +1504,9 @@ constexpr uint32_t kPoolDiv = QPP_POOL_DIV;
 #ifndef QPP_POOL512
 #define QPP_POOL512 0  // study switch: the item pool for the 512-thread shape too
 #endif
+#ifndef QPP_COMBO_PRIO
+#define QPP_COMBO_PRIO 0  // study switch: 512-thread shape, share level + item progress in one priority
+#endif
 #ifndef QPP_SHARE_PRIO
 #define QPP_SHARE_PRIO 0  // study switch: 512-thread shape, issue priority by the workgroup's share left
 #endif
@@ -1570,6 +1583,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             if (q >= pool_n) break;
             j = ib + stat + q;
         }
+#if QPP_COMBO_PRIO
+        uint32_t pbase = 0u;
+        if constexpr (WG == 512) pbase = (j < se && 2u * (se - j) > se - sb) ? 2u : 0u;
+#endif
 #if QPP_SHARE_PRIO
         if constexpr (WG == 512) {
             // the two workgroups of a CU progress through their shares
@@ -1649,7 +1666,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     const int hlen = P.hlen;
                     u32x4 got_tag;
                     const u32x4 tag = gcm_packet<kNR, ENC, BPL, SUITE, WG == 512 && QPP_PRIO512>(P, ks, pre.h0, rk, t1 & 3, G, sm.te, B,
-                                                                       (uint32_t)ioff, (uint32_t)ooff, got_tag);
+                                                                       (uint32_t)ioff, (uint32_t)ooff, got_tag
+#if QPP_COMBO_PRIO
+                                                                       , pbase
+#endif
+                                                                       );
                     QPP_PROBE_AT(6);
                     // everything below is re-derived after the step loop
                     const uint32_t t2 = tid_now(), p2 = pkt_of(t2);
