@@ -1781,13 +1781,13 @@ struct WaveSpan {
 };
 template <int WG, int SUITE>
 __device__ __forceinline__ WaveSpan wave_span(uint32_t n, const uint32_t *items, const uint32_t *irange,
-                                              uint32_t wv)
+                                              uint32_t wv, uint32_t blk)
 {
     constexpr uint32_t kWaves = WG / 64;
     WaveSpan w{0u, 0u, false};
     if (irange) {
         const uint32_t ib = irange[2 * SUITE], ie = irange[2 * SUITE + 1];
-        const uint32_t j0 = ib + blockIdx.x * kWaves;
+        const uint32_t j0 = ib + blk * kWaves;
         w.empty_wg = j0 >= ie;
         const uint32_t j = j0 + wv;
         if (j < ie) {
@@ -1795,7 +1795,7 @@ __device__ __forceinline__ WaveSpan wave_span(uint32_t n, const uint32_t *items,
             w.e = __builtin_amdgcn_readfirstlane(items[j + 1]);
         }
     } else {
-        const uint32_t b0 = blockIdx.x * (kWaves * 16u);
+        const uint32_t b0 = blk * (kWaves * 16u);
         w.empty_wg = b0 >= n;
         w.b = b0 + wv * 16u;
         w.e = w.b < n ? min(n, w.b + 16u) : w.b;
@@ -1804,20 +1804,15 @@ __device__ __forceinline__ WaveSpan wave_span(uint32_t n, const uint32_t *items,
 }
 
 // ChaCha20-Poly1305: no tables, so every wave runs its packets slot by slot
-// on its own, with the keys read from the slot (scalar loads).
+// on its own, with the keys read from the slot (scalar loads).  One wave
+// item W (<= 16 packets) of k_chacha.
 template <bool ENC, int WG, bool PRIO>
-__global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__restrict__ slots,
-                                                             uint32_t cap,
-                                                             const qpp_desc *__restrict__ desc,
-                                                             uint32_t n, const uint8_t *gin,
-                                                             uint8_t *gout,
-                                                             qpp_result *__restrict__ res,
-                                                             const uint32_t *__restrict__ items,
-                                                             const uint32_t *__restrict__ irange)
+__device__ __forceinline__ void chacha_wave(const WaveSpan &W, ChachaSmem<WG> &sm, const KeySlot *__restrict__ slots,
+                                            uint32_t cap, const qpp_desc *__restrict__ desc, const uint8_t *gin,
+                                            uint8_t *gout, qpp_result *__restrict__ res,
+                                            const uint32_t *__restrict__ irange)
 {
     constexpr int SUITE = QPP_CHACHA20_POLY1305;
-    const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
-    if (W.empty_wg) return;
 #ifdef QPP_CH_STAGGER
     {
         // study: waves start QPP_CH_STAGGER x 64 cycles apart by their slot in the SIMD
@@ -1828,7 +1823,6 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
     QPP_PROBE_AT(kProbeStart);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // set-up and key block: every wave at the top
     const uint32_t lim = W.e, planned = irange != nullptr;
-    __shared__ ChachaSmem<WG> sm;
     // the lane's packet and quad lane, re-derived from a fresh lane id where
     // used (held across the slot loop, the thread id is spilled at 128 VGPRs)
     auto p_now = [&]() -> uint32_t { return W.b + (lane_fresh() >> 2); };
@@ -1892,6 +1886,38 @@ __global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__rest
         last = cur;
     }
     QPP_PROBE_AT(9);
+}
+
+#ifndef QPP_CH_PERSIST
+#define QPP_CH_PERSIST 0  // study switch: > 0 = grid capped at that many rounds of resident workgroups, each looping
+#endif
+template <bool ENC, int WG, bool PRIO>
+__global__ __launch_bounds__(WG, kChachaWpe) void k_chacha(const KeySlot *__restrict__ slots,
+                                                             uint32_t cap,
+                                                             const qpp_desc *__restrict__ desc,
+                                                             uint32_t n, const uint8_t *gin,
+                                                             uint8_t *gout,
+                                                             qpp_result *__restrict__ res,
+                                                             const uint32_t *__restrict__ items,
+                                                             const uint32_t *__restrict__ irange)
+{
+    constexpr int SUITE = QPP_CHACHA20_POLY1305;
+    __shared__ ChachaSmem<WG> sm;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if QPP_CH_PERSIST
+    // study: each wave walks the blocks blockIdx.x, + gridDim.x, ... on its
+    // own (no barrier: a wave that ends its item takes the next at once)
+#pragma unroll 1
+    for (uint32_t vb = blockIdx.x;; vb += gridDim.x) {
+        const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, wv, vb);
+        if (W.empty_wg) break;
+        chacha_wave<ENC, WG, PRIO>(W, sm, slots, cap, desc, gin, gout, res, irange);
+    }
+#else
+    const WaveSpan W = wave_span<WG, SUITE>(n, items, irange, wv, blockIdx.x);
+    if (W.empty_wg) return;
+    chacha_wave<ENC, WG, PRIO>(W, sm, slots, cap, desc, gin, gout, res, irange);
+#endif
 }
 
 // ----------------------------------------------------------- lone packets --
@@ -3224,7 +3250,12 @@ static int launch_packets(bool enc, const qpp_keytab *kt, const qpp_desc *d_desc
                                d_out, d_res, lst);
         HIPCHK(hipGetLastError());
     } else if (mask & (1u << QPP_CHACHA20_POLY1305)) {
-        const dim3 grid((waves + kChachaWG / 64 - 1) / (kChachaWG / 64)), block(kChachaWG);
+        uint32_t cgrid = (waves + kChachaWG / 64 - 1) / (kChachaWG / 64);
+        if (QPP_CH_PERSIST > 0) {  // study: at most QPP_CH_PERSIST rounds of resident workgroups
+            const uint32_t resident = cu_count() * (uint32_t)(4 * kChachaWpe / (kChachaWG / 64)) * (uint32_t)QPP_CH_PERSIST;
+            cgrid = cgrid < resident ? cgrid : resident;
+        }
+        const dim3 grid(cgrid ? cgrid : 1u), block(kChachaWG);
         if (chacha_prio(waves)) {
             if (enc)
                 hipLaunchKernelGGL((k_chacha<true, kChachaWG, true>), grid, block, 0, s, kt->d_slots, kt->cap,
