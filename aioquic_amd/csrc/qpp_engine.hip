@@ -64,6 +64,9 @@ constexpr int kChStage = 4 * kChRegion;
 #ifndef QPP_CH_POLY4
 #define QPP_CH_POLY4 1  // study switch: 0 = one Horner multiply (and carry) per Poly1305 block
 #endif
+#ifndef QPP_CH_DPP_T
+#define QPP_CH_DPP_T 0  // study switch: one-round launches transpose a step's output blocks by DPP
+#endif
 #ifndef QPP_CH_DIRECT_ST
 #define QPP_CH_DIRECT_ST 0  // study switch: 1 = each lane stores its own blocks (no LDS round trip back)
 #endif
@@ -1071,6 +1074,9 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         QPP_PROBE_AT(5);  // the wait for this step's input (and the last step's stores)
         uint8_t *mine = stage + sub * kChRegion + qoff;
+#if QPP_CH_DPP_T
+        u32x4 o4[4];
+#endif
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const int i = 4 * c + b;
@@ -1095,7 +1101,13 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
                 }
             }
             if (valid && ENC && P.hp && i < 2) *(u32x4 *)(scr + 16 * i) = x[b];
-#if QPP_CH_DIRECT_ST
+#if QPP_CH_DPP_T
+            if constexpr (PRIO) {
+                o4[b] = o;  // transposed across the quad below, no LDS round trip
+            } else {
+                *(u32x4 *)(mine + 16 * b) = o;
+            }
+#elif QPP_CH_DIRECT_ST
             {
                 // the lane's own full block straight out (a quad's 4 stores
                 // of one instruction are 64 B apart; the 4 instructions
@@ -1107,7 +1119,58 @@ __device__ void chacha_packet(Pkt &P, const KeySlot *ks, int sub, uint8_t *scr, 
             *(u32x4 *)(mine + 16 * b) = o;
 #endif
         }
-#if QPP_CH_DIRECT_ST
+#if QPP_CH_DPP_T
+        if constexpr (PRIO) {
+            // one-round launches (latency-bound, VALU to spare): the quad's
+            // 4x4 transpose of blocks in registers, two DPP butterflies
+            // (lanes j^1, then j^2; each lane sends the block it replaces),
+            // so o4[t] = lane t's block `sub` = this lane's block of chunk
+            // 4k - 1 + t, for the same coalesced stores without writing the
+            // blocks back through LDS and reading them again
+            const bool p0 = (sub & 1) != 0, p1 = (sub & 2) != 0;
+#pragma unroll
+            for (int a = 0; a < 4; a += 2) {
+                const u32x4 snd = p0 ? o4[a] : o4[a + 1];
+                const u32x4 rcv = u32x4{quad_dpp<0xB1>(snd.x), quad_dpp<0xB1>(snd.y), quad_dpp<0xB1>(snd.z),
+                                        quad_dpp<0xB1>(snd.w)};
+                if (p0) o4[a] = rcv;
+                else o4[a + 1] = rcv;
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const u32x4 snd = p1 ? o4[a] : o4[a + 2];
+                const u32x4 rcv = u32x4{quad_dpp<0x4E>(snd.x), quad_dpp<0x4E>(snd.y), quad_dpp<0x4E>(snd.z),
+                                        quad_dpp<0x4E>(snd.w)};
+                if (p1) o4[a] = rcv;
+                else o4[a + 2] = rcv;
+            }
+            // the xor consumed every lane's input: the regions are free
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            QPP_PROBE_AT(6);  // (probe build) xor and transpose
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = 4 * (4 * k - 1 + t) + sub;
+                const uint32_t so = (i >= 0 && 16 * i + 16 <= P.clen && !tiny) ? ooff + (uint32_t)(P.hlen + 16 * i) : kOob;
+                __builtin_amdgcn_raw_buffer_store_b128(o4[t], B.out, (int)so, 0, 0);
+            }
+            QPP_PROBE_AT(8);  // (probe build) the stores' issue
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            QPP_PROBE_AT(6);  // (probe build) xor through LDS
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = 4 * (4 * k - 1 + t) + sub;
+                const uint32_t so = (i >= 0 && 16 * i + 16 <= P.clen && !tiny) ? ooff + (uint32_t)(P.hlen + 16 * i) : kOob;
+                const u32x4 v = *(const u32x4 *)(stage + t * kChRegion + qoff + 16 * sub);
+                __builtin_amdgcn_raw_buffer_store_b128(v, B.out, (int)so, 0, 0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            QPP_PROBE_AT(8);  // (probe build) the stores' reads and issue
+        }
+#elif QPP_CH_DIRECT_ST
         // the xor consumed every lane's input: the regions are free for the
         // next step's DMA
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
